@@ -1,0 +1,186 @@
+"""Benchmark: rays/s of the MI355X NeRF render path at 800x600, 128 samples/ray.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it
+is launched by torch.distributed.run, one process per GPU (RCCL).  A step is one
+``render_image`` of the full 800x600 frame at 128 uniform samples per ray on the
+fine network (the reference benchmark's semantics, ``benchmark_suite.py:151-235``;
+rays/s = W*H / time, ``:216-220``).  With N GPUs each rank renders its row band and
+the bands are all-gathered over RCCL (strong scaling: the frame is fixed).
+
+Rank 0 prints one JSON line.  ``roofline`` is the fine-MLP kernel's algorithmic
+FLOP rate (W*H_band*S*1,055,744 FLOP per launch, HIP events on the launch stream)
+against the dense MFMA peak of the compute dtype.  ``cpu_baseline`` times the
+oracle (a PyTorch-CPU restatement of the reference renderer) on a bounded row band
+of the same frame, on this node's host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "nerf-dbr_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+METRIC = "rays/sec at 800x600x128spp (render_image, fine net, uniform samples)"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--width", type=int, default=800)
+    ap.add_argument("--height", type=int, default=600)
+    ap.add_argument("--spp", type=int, default=128)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0: skip)")
+    ap.add_argument("--no-error-check", action="store_true", help="skip the bf16-vs-fp32 error band")
+    return ap.parse_args()
+
+
+def cpu_baseline(pose, width, height, spp, target_s):
+    """Oracle (PyTorch CPU) on a band of rows of the same frame; ~target_s seconds of CPU work."""
+    import torch
+
+    from nerf_amd import weights as W
+    from oracle import nerf_oracle as O
+
+    _, fine = W.synthetic_models(0)
+    net = O.Net(fine)
+    r0 = height // 2
+    t0 = time.time()
+    O.render_image(net, pose, (width, height), spp, rows=(r0, r0 + 2))
+    per_row = (time.time() - t0) / 2
+    rows = max(2, min(height - r0, int(target_s / max(per_row, 1e-6))))
+    t0 = time.time()
+    O.render_image(net, pose, (width, height), spp, rows=(r0, r0 + rows))
+    dt = time.time() - t0
+    return {"value": rows * width / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle render_image rows [{r0},{r0 + rows}) of {width}x{height}x{spp} "
+                      f"({rows * width} rays, {dt:.1f} s, 512-ray chunks, torch {torch.__version__})"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from nerf_amd import distributed as D
+    from nerf_amd import weights as W
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    width, height, spp = args.width, args.height, args.spp
+    ckpt_dir = tempfile.mkdtemp(prefix=f"nerf_bench_r{rank}_")
+    ckpt = W.write_synthetic_checkpoint(os.path.join(ckpt_dir, "synthetic.pth"), seed=0)
+    r = MI355XRenderer(args.precision, device_index=local)
+    r.setup(ckpt)
+    r.hip.set_profiling(True)
+
+    pose = torch.eye(4)            # benchmark_suite.generate_test_poses view 0
+    pose[2, 3] = 4.0
+    r0, r1 = D.band(rank, world, height)
+    band_rays = (r1 - r0) * width
+    rgb_b = torch.empty(r1 - r0, width, 3, device="cuda")
+    dep_b = torch.empty(r1 - r0, width, device="cuda")
+
+    def step():
+        r.render_rows(pose, (width, height), spp, r0, r1, rgb_b, dep_b)
+        if world > 1:
+            D.gather_bands(rgb_b, dep_b, width, height)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    mlp_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        mlp_ms.append(r.hip.stage_ms()["fine_mlp"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = 1000.0 * elapsed / args.steps
+    value = width * height * args.steps / elapsed
+
+    flop_launch = band_rays * spp * W.FLOPS_PER_SAMPLE
+    kern_ms = float(np.mean(mlp_ms))
+    achieved = flop_launch / (kern_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
+
+    extra = {}
+    if rank == 0 and args.precision == "bf16" and not args.no_error_check:
+        # bf16 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
+        ref = MI355XRenderer("fp32", device_index=local)
+        ref.setup(ckpt)
+        a0, a1 = height // 2 - 8, height // 2 + 8
+        rgb32, d32 = ref.render_rows(pose, (width, height), spp, a0, a1)
+        rgb16, d16 = r.render_rows(pose, (width, height), spp, a0, a1)
+        extra["bf16_vs_fp32_rgb_max_abs"] = float((rgb16 - rgb32).abs().max())
+        extra["bf16_vs_fp32_depth_max_abs"] = float((d16 - d32).abs().max())
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ref.render_rows(pose, (width, height), spp, 0, height)
+        torch.cuda.synchronize()
+        extra["fp32_path_rays_per_s_1gpu"] = width * height / (time.perf_counter() - t1)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(pose, width, height, spp, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic: conditioned random-init NeRFModel weights (numpy seed 0), suite pose view 0",
+            "config": {"workload": f"render_image {width}x{height}, {spp} uniform samples/ray, fine net",
+                       "resolution": [width, height], "samples_per_ray": spp,
+                       "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None,
+                         "kernel": f"mlp_{args.precision}_kernel", "kernel_ms": kern_ms,
+                         "flop_per_launch": flop_launch},
+            "cpu_baseline": cpu,
+        }
+        out.update(extra)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

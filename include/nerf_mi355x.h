@@ -1,0 +1,138 @@
+/*
+ * nerf_mi355x.h -- C ABI of the MI355X (gfx950) NeRF render path.
+ *
+ * One shared library, libnerf_mi355x.so, built from nerf-dbr_amd/csrc.  Plain
+ * pointers and sizes only: no C++ types, no torch types, no exceptions cross
+ * this boundary.  Every int-returning call returns NERF_OK (0) or a negative
+ * NERF_E_* code; the message of the last failure on the calling thread is in
+ * nerf_last_error().
+ *
+ * Device pointers are HIP device memory on the context's device; `stream` is a
+ * hipStream_t (NULL = the legacy default stream).  Calls on one context are
+ * serialised on the caller's stream; the context owns its packed weights and
+ * its scratch, the caller owns every input/output buffer.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to dgsmith7/nerf-dbr).
+ */
+#ifndef NERF_MI355X_H
+#define NERF_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NERF_ABI_VERSION 1
+
+enum nerf_status {
+  NERF_OK = 0,
+  NERF_E_INVALID = -1,    /* bad argument (shape, pointer, enum)            */
+  NERF_E_HIP = -2,        /* a HIP runtime call failed                      */
+  NERF_E_NO_WEIGHTS = -3, /* the requested network has not been loaded      */
+  NERF_E_NO_DEVICE = -4,  /* no gfx950 device at that ordinal               */
+};
+
+enum nerf_precision {
+  NERF_FP32 = 0, /* f32-in MFMA (v_mfma_f32_32x32x2_f32); the parity path   */
+  NERF_BF16 = 1, /* bf16-in MFMA (v_mfma_f32_32x32x16_bf16), f32 accumulate */
+};
+
+enum nerf_net { NERF_NET_COARSE = 0, NERF_NET_FINE = 1 };
+
+/* Number of parameter tensors of one NeRFModel, in state-dict order:
+ * layers.0..7, density_head, color_layers.0, color_layers.1 -- (weight, bias)
+ * each, weight in nn.Linear [out, in] row-major fp32 (src/models/nerf.py:72-90). */
+#define NERF_N_PARAMS 22
+
+typedef struct nerf_ctx nerf_ctx;
+
+int nerf_abi_version(void);
+const char* nerf_last_error(void);
+
+/* Replaces: BaseUnifiedRenderer.__init__ device binding (src/benchmark/base_renderer.py:93-112). */
+int nerf_ctx_create(int device, nerf_ctx** out);
+void nerf_ctx_destroy(nerf_ctx* ctx);
+int nerf_device_name(int device, char* buf, int buf_len);
+
+/* Replaces: SharedNeRFModel.load_models (src/benchmark/base_renderer.py:28-78) --
+ * the caller has already read the checkpoint; this packs the 22 host tensors
+ * into the kernels' fragment layouts and uploads them once.  Host buffers may
+ * be freed after the call returns. */
+int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, int n_params);
+
+/* Pure host helper (no device needed): packs one network into the three blobs
+ * the kernels read.  Sizes in bytes via nerf_packed_sizes.  Used by the
+ * loader above and by host-side layout tests. */
+void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob);
+int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob, uint16_t* bf16_blob,
+                      float* param_blob);
+
+/* Pure host helper: z = near*(1-t) + far*t in fp32, operation for operation
+ * (src/benchmark/base_renderer.py:274-275). */
+void nerf_uniform_z(const float* t_vals, int n, float near_, float far_, float* z_out);
+
+/* Replaces: BaseUnifiedRenderer.generate_rays (src/benchmark/base_renderer.py:223-258)
+ * for image rows [row0, row1).  c2w: 16 floats row-major [4][4] (host).  Outputs are
+ * device [(row1-row0)*width][3] fp32. */
+int nerf_generate_rays(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1,
+                       float focal, float* rays_o, float* rays_d, void* stream);
+
+/* Replaces: BaseUnifiedRenderer.sample_points_on_rays + query_nerf_networks +
+ * NeRFModel.forward (base_renderer.py:165-188, 260-281; src/models/nerf.py:92-131)
+ * fused: sample s of ray r sits at  o_r + d_r * z[r*z_ray_stride + s]  (z_ray_stride 0:
+ * one shared [n_samples] table), is encoded, and runs through the whole MLP.
+ * out: device [n_rays*n_samples][4] = (sigma, r, g, b). */
+int nerf_mlp_forward(nerf_ctx* ctx, int net, int precision, const float* rays_o, const float* rays_d,
+                     const float* z, int z_ray_stride, int n_rays, int n_samples, float* out,
+                     void* stream);
+
+/* Replaces: query_nerf_networks on explicit point/direction lists
+ * (base_renderer.py:165-188): positions, directions device [n][3] ->
+ * out device [n][4] = (sigma, r, g, b). */
+int nerf_query(nerf_ctx* ctx, int net, int precision, const float* positions, const float* directions,
+               int n, float* out, void* stream);
+
+/* Replaces: PyTorchCPURenderer.execute_volume_rendering (src/benchmark/pytorch_renderers.py:105-125)
+ * and VolumeRenderer.volume_render (src/utils/rendering.py:102-143).
+ * sigma[(r*S+s)*sigma_stride], rgb[(r*S+s)*rgb_stride + c], z[r*z_ray_stride + s],
+ * rays_d[r*3 + c].  Outputs device: rgb_out [n_rays][3], depth_out [n_rays]; acc_out
+ * [n_rays] and weights_out [n_rays][S] may be NULL. */
+int nerf_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride,
+                   const float* z, int z_ray_stride, const float* rays_d, int n_rays, int n_samples,
+                   float* rgb_out, float* depth_out, float* acc_out, float* weights_out, void* stream);
+
+/* Replaces (and fixes): VolumeRenderer.importance_sample (src/utils/rendering.py:54-100),
+ * which crashes at its gather (:89-90).  For each ray: pdf from weights+1e-5 (sequential
+ * normaliser), cdf, inverse-cdf samples at u (u[r*u_ray_stride + k], ascending per ray),
+ * then the sorted union with the coarse z.  z_fine: device [n_rays][n_coarse+n_importance]. */
+int nerf_importance_sample(const float* z_coarse, int z_ray_stride, const float* weights,
+                           const float* u, int u_ray_stride, int n_rays, int n_coarse,
+                           int n_importance, float* z_fine, void* stream);
+
+/* Replaces: PyTorchCPURenderer.render_image (src/benchmark/pytorch_renderers.py:127-154)
+ * for rows [row0, row1) of a width x height image, the whole path in one call:
+ * rays -> (coarse pass + importance samples if n_importance > 0) -> fine pass -> composite.
+ * t_vals: host [n_samples] = torch.linspace(0,1,n_samples) bits (the reference's table).
+ * u: host [n_importance] ascending draw shared by every ray (NULL: t-table style
+ * linspace(0,1,n_importance) computed as (k/(n-1)) in fp32).  With n_importance > 0,
+ * n_samples is the coarse count.  rgb_out device [(row1-row0)*width][3], depth_out
+ * device [(row1-row0)*width]. */
+int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1,
+                float focal, float near_, float far_, const float* t_vals, int n_samples,
+                int n_importance, const float* u, int precision, float* rgb_out, float* depth_out,
+                void* stream);
+
+/* Per-stage device time of the last nerf_render on this context, from HIP events
+ * recorded on the caller's stream when profiling is on.  Stages:
+ * 0 rays, 1 coarse MLP, 2 importance, 3 fine MLP, 4 composite. */
+#define NERF_N_STAGES 5
+int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable);
+int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out /* [NERF_N_STAGES] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NERF_MI355X_H */

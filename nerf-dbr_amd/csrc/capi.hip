@@ -1,0 +1,332 @@
+// C ABI of libnerf_mi355x.so (declared in include/nerf_mi355x.h).
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "nerf_device.h"
+#include "nerf_internal.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+}  // namespace
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                                 \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) return set_error(NERF_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                           __FILE__, __LINE__);                                      \
+  } while (0)
+
+using namespace nerf;
+
+struct NetDev {
+  float* f32 = nullptr;
+  void* bf16 = nullptr;
+  float* params = nullptr;
+  bool loaded = false;
+};
+
+struct nerf_ctx {
+  int device = 0;
+  NetDev net[2];
+  // scratch, grown on demand and reused across renders
+  float* rays = nullptr;       // [2][n_rays][3] (o then d)
+  size_t rays_cap = 0;         // rays
+  float* mlp_out = nullptr;    // [P][4]
+  size_t mlp_cap = 0;          // points
+  float* zbuf = nullptr;       // coarse table [S] + per-ray fine z [R][S+N]
+  size_t z_cap = 0;            // floats
+  float* wbuf = nullptr;       // coarse weights [R][S] + u [N]
+  size_t w_cap = 0;            // floats
+  float* host_stage = nullptr; // pinned: z table + u
+  bool profiling = false;
+  hipEvent_t ev[NERF_N_STAGES + 1] = {};
+  bool stage_ran[NERF_N_STAGES] = {};
+};
+
+namespace {
+
+template <typename T>
+int grow(T*& p, size_t& cap, size_t need, const char* what) {
+  if (need <= cap) return NERF_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t n = need + need / 8;
+  hipError_t e = hipMalloc((void**)&p, n * sizeof(T));
+  if (e != hipSuccess) return set_error(NERF_E_HIP, "hipMalloc %s (%zu bytes): %s", what, n * sizeof(T), hipGetErrorString(e));
+  cap = n;
+  return NERF_OK;
+}
+
+int check_net(nerf_ctx* ctx, int net, int precision) {
+  if (!ctx) return set_error(NERF_E_INVALID, "null context");
+  if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
+  if (precision != NERF_FP32 && precision != NERF_BF16) return set_error(NERF_E_INVALID, "bad precision %d", precision);
+  if (!ctx->net[net].loaded) return set_error(NERF_E_NO_WEIGHTS, "%s network not loaded", net ? "fine" : "coarse");
+  return NERF_OK;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, long n, float* out, bool expl,
+                   hipStream_t s) {
+  const NetDev& nd = ctx->net[net];
+  if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s);
+  return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nerf_abi_version(void) { return NERF_ABI_VERSION; }
+const char* nerf_last_error(void) { return g_err; }
+
+int nerf_device_name(int device, char* buf, int buf_len) {
+  if (!buf || buf_len <= 0) return set_error(NERF_E_INVALID, "bad buffer");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  snprintf(buf, size_t(buf_len), "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
+  return NERF_OK;
+}
+
+int nerf_ctx_create(int device, nerf_ctx** out) {
+  if (!out) return set_error(NERF_E_INVALID, "null out pointer");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+    return set_error(NERF_E_NO_DEVICE, "no HIP device %d (count %d)", device, n);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_error(NERF_E_NO_DEVICE, "device %d is %s; this library is built for gfx950 (MI355X)", device,
+                     prop.gcnArchName);
+  DeviceGuard g(device);
+  nerf_ctx* ctx = new nerf_ctx();
+  ctx->device = device;
+  for (auto& e : ctx->ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipHostMalloc((void**)&ctx->host_stage, sizeof(float) * 2048, hipHostMallocDefault));
+  *out = ctx;
+  return NERF_OK;
+}
+
+void nerf_ctx_destroy(nerf_ctx* ctx) {
+  if (!ctx) return;
+  DeviceGuard g(ctx->device);
+  (void)hipDeviceSynchronize();
+  for (auto& nd : ctx->net) {
+    if (nd.f32) (void)hipFree(nd.f32);
+    if (nd.bf16) (void)hipFree(nd.bf16);
+    if (nd.params) (void)hipFree(nd.params);
+  }
+  for (float* p : {ctx->rays, ctx->mlp_out, ctx->zbuf, ctx->wbuf})
+    if (p) (void)hipFree(p);
+  if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete ctx;
+}
+
+int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, int n_params) {
+  if (!ctx) return set_error(NERF_E_INVALID, "null context");
+  if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
+  size_t nf32, nbf16, nprm;
+  nerf_packed_sizes(&nf32, &nbf16, &nprm);
+  std::vector<float> f32(nf32 / 4), prm(nprm / 4);
+  std::vector<uint16_t> bf(nbf16 / 2);
+  int rc = nerf_pack_weights(params, n_params, f32.data(), bf.data(), prm.data());
+  if (rc != NERF_OK) return rc;
+  DeviceGuard g(ctx->device);
+  NetDev& nd = ctx->net[net];
+  if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
+  if (!nd.bf16) HIP_TRY(hipMalloc(&nd.bf16, nbf16));
+  if (!nd.params) HIP_TRY(hipMalloc((void**)&nd.params, nprm));
+  HIP_TRY(hipMemcpy(nd.f32, f32.data(), nf32, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(nd.bf16, bf.data(), nbf16, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));
+  nd.loaded = true;
+  return NERF_OK;
+}
+
+int nerf_generate_rays(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal,
+                       float* rays_o, float* rays_d, void* stream) {
+  if (!ctx || !c2w || !rays_o || !rays_d) return set_error(NERF_E_INVALID, "nerf_generate_rays: null argument");
+  if (width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 > row1)
+    return set_error(NERF_E_INVALID, "nerf_generate_rays: bad image/rows %dx%d [%d,%d)", width, height, row0, row1);
+  DeviceGuard g(ctx->device);
+  HIP_TRY(launch_generate_rays(c2w, width, height, row0, row1, focal, rays_o, rays_d, (hipStream_t)stream));
+  return NERF_OK;
+}
+
+int nerf_mlp_forward(nerf_ctx* ctx, int net, int precision, const float* rays_o, const float* rays_d, const float* z,
+                     int z_ray_stride, int n_rays, int n_samples, float* out, void* stream) {
+  int rc = check_net(ctx, net, precision);
+  if (rc != NERF_OK) return rc;
+  if (n_rays < 0 || n_samples <= 0 || z_ray_stride < 0) return set_error(NERF_E_INVALID, "nerf_mlp_forward: bad sizes");
+  if (n_rays == 0) return NERF_OK;
+  if (!rays_o || !rays_d || !z || !out) return set_error(NERF_E_INVALID, "nerf_mlp_forward: null pointer");
+  DeviceGuard g(ctx->device);
+  SampleSrc src{rays_o, rays_d, z, z_ray_stride, n_samples, nullptr, nullptr};
+  HIP_TRY(run_mlp(ctx, net, precision, src, long(n_rays) * n_samples, out, false, (hipStream_t)stream));
+  return NERF_OK;
+}
+
+int nerf_query(nerf_ctx* ctx, int net, int precision, const float* positions, const float* directions, int n,
+               float* out, void* stream) {
+  int rc = check_net(ctx, net, precision);
+  if (rc != NERF_OK) return rc;
+  if (n < 0) return set_error(NERF_E_INVALID, "nerf_query: n < 0");
+  if (n == 0) return NERF_OK;
+  if (!positions || !directions || !out) return set_error(NERF_E_INVALID, "nerf_query: null pointer");
+  DeviceGuard g(ctx->device);
+  SampleSrc src{nullptr, nullptr, nullptr, 0, 1, positions, directions};
+  HIP_TRY(run_mlp(ctx, net, precision, src, n, out, true, (hipStream_t)stream));
+  return NERF_OK;
+}
+
+int nerf_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride, const float* z,
+                   int z_ray_stride, const float* rays_d, int n_rays, int n_samples, float* rgb_out, float* depth_out,
+                   float* acc_out, float* weights_out, void* stream) {
+  if (n_rays < 0 || n_samples <= 0) return set_error(NERF_E_INVALID, "nerf_composite: bad sizes");
+  if (n_rays == 0) return NERF_OK;
+  if (!sigma || !rgb || !z || !rays_d || !rgb_out || !depth_out) return set_error(NERF_E_INVALID, "nerf_composite: null pointer");
+  HIP_TRY(launch_composite(sigma, sigma_stride, rgb, rgb_stride, z, z_ray_stride, rays_d, n_rays, n_samples, rgb_out,
+                           depth_out, acc_out, weights_out, (hipStream_t)stream));
+  return NERF_OK;
+}
+
+int nerf_importance_sample(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
+                           int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine, void* stream) {
+  if (n_rays < 0 || n_coarse <= 0 || n_coarse > 256 || n_importance < 0)
+    return set_error(NERF_E_INVALID, "nerf_importance_sample: bad sizes (n_coarse must be 1..256)");
+  if (n_rays == 0) return NERF_OK;
+  if (!z_coarse || !weights || !z_fine || (n_importance > 0 && !u))
+    return set_error(NERF_E_INVALID, "nerf_importance_sample: null pointer");
+  HIP_TRY(launch_importance(z_coarse, z_ray_stride, weights, u, u_ray_stride, n_rays, n_coarse, n_importance, z_fine,
+                            (hipStream_t)stream));
+  return NERF_OK;
+}
+
+int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable) {
+  if (!ctx) return set_error(NERF_E_INVALID, "null context");
+  ctx->profiling = enable != 0;
+  return NERF_OK;
+}
+
+int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out) {
+  if (!ctx || !ms_out) return set_error(NERF_E_INVALID, "null argument");
+  DeviceGuard g(ctx->device);
+  HIP_TRY(hipEventSynchronize(ctx->ev[NERF_N_STAGES]));
+  for (int i = 0; i < NERF_N_STAGES; ++i) {
+    ms_out[i] = 0.0f;
+    if (ctx->profiling && ctx->stage_ran[i]) HIP_TRY(hipEventElapsedTime(&ms_out[i], ctx->ev[i], ctx->ev[i + 1]));
+  }
+  return NERF_OK;
+}
+
+int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal, float near_,
+                float far_, const float* t_vals, int n_samples, int n_importance, const float* u, int precision,
+                float* rgb_out, float* depth_out, void* stream) {
+  const int net_main = NERF_NET_FINE;
+  int rc = check_net(ctx, net_main, precision);
+  if (rc != NERF_OK) return rc;
+  if (n_importance > 0 && (rc = check_net(ctx, NERF_NET_COARSE, precision)) != NERF_OK) return rc;
+  if (!c2w || !t_vals || !rgb_out || !depth_out) return set_error(NERF_E_INVALID, "nerf_render: null argument");
+  if (width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 > row1)
+    return set_error(NERF_E_INVALID, "nerf_render: bad image/rows %dx%d [%d,%d)", width, height, row0, row1);
+  if (n_samples <= 0 || n_samples > 1024 || n_importance < 0 || n_importance > 1024 ||
+      (n_importance > 0 && n_samples > 256))
+    return set_error(NERF_E_INVALID, "nerf_render: bad sample counts %d+%d", n_samples, n_importance);
+  const long n_rays = long(row1 - row0) * width;
+  if (n_rays == 0) return NERF_OK;
+  const int n_fine = n_samples + n_importance;
+  if (n_rays * n_fine > 0x7FFFFFFFL * 128L) return set_error(NERF_E_INVALID, "nerf_render: too many samples");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+
+  // z table (base_renderer.py:274-275) and the importance draw, via pinned staging
+  HIP_TRY(hipStreamSynchronize(s));   // host_stage may still feed a previous copy
+  float* hz = ctx->host_stage;
+  nerf_uniform_z(t_vals, n_samples, near_, far_, hz);
+  float* hu = hz + 1024;
+  for (int k = 0; k < n_importance; ++k)
+    hu[k] = u ? u[k] : (n_importance > 1 ? float(k) / float(n_importance - 1) : 0.0f);
+
+  if ((rc = grow(ctx->rays, ctx->rays_cap, size_t(n_rays) * 6, "rays")) != NERF_OK) return rc;
+  if ((rc = grow(ctx->mlp_out, ctx->mlp_cap, size_t(n_rays) * n_fine * 4, "mlp_out")) != NERF_OK) return rc;
+  const size_t zfloats = 1024 + (n_importance > 0 ? size_t(n_rays) * n_fine : 0);
+  if ((rc = grow(ctx->zbuf, ctx->z_cap, zfloats, "z")) != NERF_OK) return rc;
+  const size_t wfloats = 1024 + (n_importance > 0 ? size_t(n_rays) * n_samples : 0);
+  if ((rc = grow(ctx->wbuf, ctx->w_cap, wfloats, "weights")) != NERF_OK) return rc;
+
+  float* d_ztab = ctx->zbuf;
+  float* d_zfine = ctx->zbuf + 1024;
+  float* d_u = ctx->wbuf;
+  float* d_w = ctx->wbuf + 1024;
+  float* rays_o = ctx->rays;
+  float* rays_d = ctx->rays + n_rays * 3;
+  HIP_TRY(hipMemcpyAsync(d_ztab, hz, sizeof(float) * n_samples, hipMemcpyHostToDevice, s));
+  if (n_importance > 0) HIP_TRY(hipMemcpyAsync(d_u, hu, sizeof(float) * n_importance, hipMemcpyHostToDevice, s));
+
+  for (bool& b : ctx->stage_ran) b = false;
+  auto mark = [&](int i) -> int {
+    if (ctx->profiling) HIP_TRY(hipEventRecord(ctx->ev[i], s));
+    return NERF_OK;
+  };
+  if ((rc = mark(0)) != NERF_OK) return rc;
+  HIP_TRY(launch_generate_rays(c2w, width, height, row0, row1, focal, rays_o, rays_d, s));
+  ctx->stage_ran[0] = true;
+  if ((rc = mark(1)) != NERF_OK) return rc;
+  const float* z_main = d_ztab;
+  int z_stride = 0;
+  if (n_importance > 0) {
+    SampleSrc src{rays_o, rays_d, d_ztab, 0, n_samples, nullptr, nullptr};
+    HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s));
+    ctx->stage_ran[1] = true;
+    if ((rc = mark(2)) != NERF_OK) return rc;
+    // coarse weights only (the coarse image itself is not an output of render_image)
+    HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, d_ztab, 0, rays_d, int(n_rays), n_samples,
+                             rgb_out, depth_out, nullptr, d_w, s));
+    HIP_TRY(launch_importance(d_ztab, 0, d_w, d_u, 0, int(n_rays), n_samples, n_importance, d_zfine, s));
+    ctx->stage_ran[2] = true;
+    z_main = d_zfine;
+    z_stride = n_fine;
+  } else {
+    if ((rc = mark(2)) != NERF_OK) return rc;
+  }
+  if ((rc = mark(3)) != NERF_OK) return rc;
+  {
+    SampleSrc src{rays_o, rays_d, z_main, z_stride, n_fine, nullptr, nullptr};
+    HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s));
+    ctx->stage_ran[3] = true;
+  }
+  if ((rc = mark(4)) != NERF_OK) return rc;
+  HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_main, z_stride, rays_d, int(n_rays), n_fine,
+                           rgb_out, depth_out, nullptr, nullptr, s));
+  ctx->stage_ran[4] = true;
+  HIP_TRY(hipEventRecord(ctx->ev[NERF_N_STAGES], s));
+  return NERF_OK;
+}
+
+}  // extern "C"

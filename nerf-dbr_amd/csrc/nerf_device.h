@@ -1,0 +1,166 @@
+// Device helpers shared by the gfx950 NeRF kernels: exact-order sampling,
+// positional encoding into per-lane-half slots, and the VALU heads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nerf_layout.h"
+
+namespace nerf {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// fl32(2^k * pi): `freq * torch.pi` with freq = 2.0**k as fp32 (nerf.py:22,42);
+// a power-of-two multiple of fl32(pi), so exact.
+__device__ __forceinline__ float pe_coef(int k) { return __builtin_ldexpf(3.14159274101257324f, k); }
+
+// base_renderer.py:279: o + d*z as a rounded multiply, then a rounded add.
+__device__ __forceinline__ float sample_coord(float o, float d, float z) {
+  return __fadd_rn(o, __fmul_rn(d, z));
+}
+
+// Position encoding slots of lane half h (nerf_layout.h pe_slot_feature):
+// 15 sin/cos pairs + the raw coordinates it owns.  Accurate sincosf (ocml),
+// never the hardware v_sin/v_cos approximations.
+__device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, float (&pe)[32]) {
+#pragma unroll
+  for (int kk = 0; kk < 5; ++kk) {
+    const float c = pe_coef(5 * h + kk);
+    const float xs[3] = {x0, x1, x2};
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float s, co;
+      sincosf(__fmul_rn(c, xs[m]), &s, &co);
+      pe[6 * kk + m] = s;
+      pe[6 * kk + 3 + m] = co;
+    }
+  }
+  pe[30] = h ? x2 : x0;
+  pe[31] = h ? 0.0f : x1;
+}
+
+__device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, float (&de)[16]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const float c = pe_coef(2 * h + kk);
+    const float ds[3] = {d0, d1, d2};
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float s, co;
+      sincosf(__fmul_rn(c, ds[m]), &s, &co);
+      de[6 * kk + m] = s;
+      de[6 * kk + 3 + m] = co;
+    }
+  }
+  de[12] = h ? d2 : d0;
+  de[13] = h ? 0.0f : d1;
+  de[14] = 0.0f;
+  de[15] = 0.0f;
+}
+
+__device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
+
+// torch.sigmoid: 1 / (1 + exp(-x))
+__device__ __forceinline__ float sigmoid_ref(float x) { return __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-x))); }
+
+// Density (nerf.py:114) and colour-1 + sigmoid (nerf.py:123-129) from the
+// ReLU'd fp32 accumulators.  prm points at the params blob (LDS or global).
+// Each lane sums its 128 (resp. 64) rows; the two lane halves of a column then
+// add through a cross-half swap.
+template <typename PTR>
+__device__ __forceinline__ float density_head(const f32x16 (&x)[8], PTR prm, int h) {
+  float part = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    asm volatile("" ::: "memory");   // keep one tile of weights in flight, not all 128
+    const f32x4* w4 = (const f32x4*)(prm + kSigW + (h * 8 + t) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = w4[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part = fmaf(w[i], x[t][4 * q + i], part);
+    }
+  }
+  const float tot = part + __shfl_xor(part, 32);
+  return relu(tot + prm[kSigB]);
+}
+
+template <typename PTR>
+__device__ __forceinline__ void color_head(const f32x16 (&hc)[8], PTR prm, int h, float (&rgb)[3]) {  // tiles 0..3
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float part = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      asm volatile("" ::: "memory");
+      const f32x4* w4 = (const f32x4*)(prm + kC1W + ((c * 2 + h) * 4 + t) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 w = w4[q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part = fmaf(w[i], hc[t][4 * q + i], part);
+      }
+    }
+    const float tot = part + __shfl_xor(part, 32);
+    rgb[c] = sigmoid_ref(tot + prm[kC1B + c]);
+  }
+}
+
+// Bias pre-load: accumulator register r of tile o for lane half h.
+template <int NT, typename PTR>
+__device__ __forceinline__ void load_bias(f32x16 (&acc)[8], PTR prm, int layer, int h) {
+#pragma unroll
+  for (int o = 0; o < NT; ++o) {
+    const f32x4* b4 = (const f32x4*)(prm + kBiasOff + 256 * layer + (o * 2 + h) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 b = b4[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[o][4 * q + i] = b[i];
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void relu_tiles(f32x16 (&acc)[8]) {
+#pragma unroll
+  for (int o = 0; o < NT; ++o)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[o][r] = relu(acc[o][r]);
+}
+
+// Where a wave's 32 sample columns come from.
+struct SampleSrc {
+  const float* rays_o;     // [n_rays][3]        (mode 0)
+  const float* rays_d;     // [n_rays][3]
+  const float* z;          // z[ray*z_stride + s]
+  int z_stride;
+  int n_samples;
+  const float* points;     // [P][3]             (mode 1: explicit points)
+  const float* dirs;       // [P][3]
+};
+
+// Fetch the sample point and its view direction for sample p.
+template <bool kExplicit>
+__device__ __forceinline__ void fetch_sample(const SampleSrc& src, long p, float (&x)[3], float (&d)[3]) {
+  if (kExplicit) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      x[c] = src.points[3 * p + c];
+      d[c] = src.dirs[3 * p + c];
+    }
+  } else {
+    const long ray = p / src.n_samples;
+    const long s = p - ray * src.n_samples;
+    const float zz = src.z[ray * src.z_stride + s];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      d[c] = src.rays_d[3 * ray + c];
+      x[c] = sample_coord(src.rays_o[3 * ray + c], d[c], zz);
+    }
+  }
+}
+
+}  // namespace nerf

@@ -1,0 +1,28 @@
+// Internal declarations shared by the C ABI (capi.hip), the packer and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "nerf_mi355x.h"
+
+// Record a failure for nerf_last_error() (thread-local) and return `code`.
+int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+namespace nerf {
+
+struct SampleSrc;
+
+hipError_t launch_generate_rays(const float* c2w_rowmajor16, int width, int height, int row0, int row1,
+                                float focal, float* rays_o, float* rays_d, hipStream_t stream);
+hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSrc& src, long n_points,
+                          float* out, bool explicit_points, hipStream_t stream);
+hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points,
+                           float* out, bool explicit_points, hipStream_t stream);
+hipError_t launch_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride,
+                            const float* z, int z_ray_stride, const float* rays_d, int n_rays, int n_samples,
+                            float* rgb_out, float* depth_out, float* acc_out, float* weights_out,
+                            hipStream_t stream);
+hipError_t launch_importance(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
+                             int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine,
+                             hipStream_t stream);
+
+}  // namespace nerf

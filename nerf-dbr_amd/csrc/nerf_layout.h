@@ -1,0 +1,137 @@
+// Shared host/device description of the NeRF MLP as the gfx950 kernels see it.
+//
+// The network is the reference NeRFModel (src/models/nerf.py:48-131).  Kernels
+// compute every Linear in the transposed orientation
+//     H^T[out_feature, sample] = W[out, k] . X^T[k, sample]
+// with 32x32 MFMA tiles: output features on the accumulator's ROW axis, samples
+// on its COLUMN (lane) axis.  The accumulator of layer l is then already the
+// B operand of layer l+1 (the contraction runs over its row index), so
+// activations never leave registers; only the weights (the A operand) stream
+// through LDS / L2.  The price is a fixed permutation of each layer's input
+// (k) order, which is absorbed into the host-side weight packing below.
+//
+// Accumulator map of v_mfma_f32_32x32x{16_bf16,2_f32} (same on gfx950):
+//     lane l, register r  ->  row (r&3) + 8*(r>>2) + 4*(l>>5),  column l&31.
+#pragma once
+
+#ifdef __HIPCC__
+#define NL_HD __host__ __device__ constexpr
+#else
+#define NL_HD constexpr
+#endif
+
+namespace nerf {
+
+constexpr int kHidden = 256;
+constexpr int kPosL = 10, kDirL = 4;
+constexpr int kPosDim = 3 + 6 * kPosL;   // 63
+constexpr int kDirDim = 3 + 6 * kDirL;   // 27
+constexpr int kColorHidden = 128;
+constexpr int kSamplesPerWave = 32;      // one 32-column MFMA tile per wave
+
+// Per-sample positional-encoding slots.  The two lane halves of a column share
+// one sample; half h computes 32 of the 64 (63 + 1 pad) position features and
+// 16 of the 32 (27 + 5 pad) direction features.  The split is chosen so that
+// every half evaluates whole sin/cos pairs: half 0 owns frequencies 0-4 plus
+// x0,x1; half 1 owns frequencies 5-9 plus x2.  Returned index is the feature's
+// position in the reference's encoding ([x, sin f0, cos f0, sin f1, ...],
+// nerf.py:40-45), or -1 for padding.
+NL_HD int pe_slot_feature(int h, int q) {   // q in [0, 32)
+  if (q < 30) return 3 + 6 * (5 * h + q / 6) + (q % 6);
+  if (h == 0) return q - 30;                // x0, x1
+  return q == 30 ? 2 : -1;                  // x2, pad
+}
+NL_HD int dpe_slot_feature(int h, int q) {  // q in [0, 16)
+  if (q < 12) return 3 + 6 * (2 * h + q / 6) + (q % 6);
+  if (h == 0) return q < 14 ? q - 12 : -1;  // d0, d1, pad, pad
+  return q == 12 ? 2 : -1;                  // d2, pad x3
+}
+
+NL_HD int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// f32 MFMA (32x32x2): k-step u feeds one value per lane half.  Hidden k-steps
+// come straight from the previous accumulator: tile u>>4, register u&15.
+NL_HD int hid_f32_feature(int u, int h) { return 32 * (u >> 4) + acc_row(u & 15, h); }
+// bf16 MFMA (32x32x16): k-step u (16 k) takes registers 8s..8s+7 of tile u>>1,
+// s = u&1, converted pairwise to bf16.  Element j of lane half h is row
+// 16s + 8(j>>2) + 4h + (j&3) of that tile.
+NL_HD int hid_bf16_feature(int u, int h, int j) {
+  return 32 * (u >> 1) + 16 * (u & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+
+// MFMA layers (density head and the last colour layer run on the VALU).
+enum LayerId { L0 = 0, L1, L2, L3, L4, L5, L6, L7, C0, kNumMfmaLayers };
+enum Extra { kNone = 0, kPos = 1, kDir = 2 };
+
+struct LayerShape {
+  int out;        // output features
+  int in;         // reference in_features
+  int hidden;     // leading hidden inputs (0 or 256)
+  int extra;      // Extra kind appended after the hidden inputs
+};
+
+NL_HD LayerShape layer_shape(int l) {
+  if (l == L0) return {kHidden, kPosDim, 0, kPos};
+  if (l == L4) return {kHidden, kHidden + kPosDim, kHidden, kPos};
+  if (l == C0) return {kColorHidden, kHidden + kDirDim, kHidden, kDir};
+  return {kHidden, kHidden, kHidden, kNone};
+}
+NL_HD int extra_slots(int kind) { return kind == kPos ? 32 : kind == kDir ? 16 : 0; }
+NL_HD int out_tiles(int l) { return layer_shape(l).out / 32; }
+NL_HD int ksteps_f32(int l) { LayerShape s = layer_shape(l); return s.hidden / 2 + extra_slots(s.extra); }
+NL_HD int ksteps_bf16(int l) { LayerShape s = layer_shape(l); return s.hidden / 16 + extra_slots(s.extra) / 8; }
+
+// Reference column index of the weight that multiplies the value lane half h
+// supplies at (k-step u, element j) -- or -1 for padding.
+NL_HD int f32_k_col(int l, int u, int h) {
+  LayerShape s = layer_shape(l);
+  int nh = s.hidden / 2;
+  if (u < nh) return hid_f32_feature(u, h);
+  int q = u - nh;
+  int f = s.extra == kPos ? pe_slot_feature(h, q) : dpe_slot_feature(h, q);
+  return f < 0 ? -1 : s.hidden + f;
+}
+NL_HD int bf16_k_col(int l, int u, int h, int j) {
+  LayerShape s = layer_shape(l);
+  int nh = s.hidden / 16;
+  if (u < nh) return hid_bf16_feature(u, h, j);
+  int q = 8 * (u - nh) + j;
+  int f = s.extra == kPos ? pe_slot_feature(h, q) : dpe_slot_feature(h, q);
+  return f < 0 ? -1 : s.hidden + f;
+}
+
+// ---------------------------------------------------------------- packing --
+// f32 A blob, per layer: [u/4][tile o][lane 64][4 floats]  (one float4 per lane
+//   covers four consecutive k-steps).
+// bf16 A blob, per layer: [u][tile o][lane 64][8 bf16]; the whole stream is cut
+//   into 16 KiB chunks consumed in order (2 k-steps of a 256-out layer, 4 of C0);
+//   C0 is zero-padded to whole chunks.
+// Params blob (fp32, shared by both precisions), in floats:
+//   bias[layer l][tile o][half h][16]  at  kBiasOff + 256*l (C0: 128 used)
+//   density weight [h][tile t][16] at kSigW, density bias at kSigB
+//   colour-1 weight [c][h][t 0..3][16] at kC1W, colour-1 bias [3] at kC1B
+constexpr int kChunkBytes = 16384;
+constexpr int kBiasOff = 0;
+constexpr int kSigW = 256 * kNumMfmaLayers;         // 2304
+constexpr int kSigB = kSigW + 256;
+constexpr int kC1W = kSigB + 4;                     // 16-B aligned
+constexpr int kC1B = kC1W + 3 * 128;
+constexpr int kParamFloats = kC1B + 4;              // 2952
+
+NL_HD int f32_layer_floats(int l) { return ksteps_f32(l) * out_tiles(l) * 64; }
+NL_HD int bf16_layer_chunks(int l) {
+  int bytes = ksteps_bf16(l) * out_tiles(l) * 1024;
+  return (bytes + kChunkBytes - 1) / kChunkBytes;
+}
+NL_HD int f32_blob_floats() {
+  int n = 0;
+  for (int l = 0; l < kNumMfmaLayers; ++l) n += f32_layer_floats(l);
+  return n;
+}
+NL_HD int bf16_blob_chunks() {
+  int n = 0;
+  for (int l = 0; l < kNumMfmaLayers; ++l) n += bf16_layer_chunks(l);
+  return n;
+}
+
+}  // namespace nerf

@@ -1,0 +1,160 @@
+// Ray generation, alpha compositing and the inverse-CDF importance sampler.
+// These are byte-light, per-ray kernels (<1% of frame time); what matters is
+// that they follow the reference's arithmetic operation for operation.
+#include "nerf_device.h"
+#include "nerf_internal.h"
+
+namespace nerf {
+namespace {
+
+struct Pose {
+  float r[9];   // camera-to-world rotation, row-major
+  float t[3];
+};
+
+// BaseUnifiedRenderer.generate_rays (base_renderer.py:223-258):
+//   dir = ((i - W*0.5)/f, -(j - H*0.5)/f, -1)  with pixel corners i, j;
+//   rays_d[k] = (dir0*R[k][0] + dir1*R[k][1]) + dir2*R[k][2]  (torch.sum order);
+//   rays_o = t.  One thread per pixel of rows [row0, row1).
+__global__ void rays_kernel(Pose pose, int width, float half_w, float half_h, float focal, int row0, long n,
+                            float* __restrict__ rays_o, float* __restrict__ rays_d) {
+  const long k = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int row = row0 + int(k / width);
+  const int col = int(k % width);
+  const float dx = __fdiv_rn(__fsub_rn(float(col), half_w), focal);
+  const float dy = -__fdiv_rn(__fsub_rn(float(row), half_h), focal);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float p0 = __fmul_rn(dx, pose.r[3 * c + 0]);
+    const float p1 = __fmul_rn(dy, pose.r[3 * c + 1]);
+    const float p2 = -pose.r[3 * c + 2];
+    rays_d[3 * k + c] = __fadd_rn(__fadd_rn(p0, p1), p2);
+    rays_o[3 * k + c] = pose.t[c];
+  }
+}
+
+// execute_volume_rendering (pytorch_renderers.py:105-125): one thread per ray,
+// transmittance as the sequential exclusive product (torch.cumprod order).
+__global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stride, const float* __restrict__ rgb,
+                                 int rgb_stride, const float* __restrict__ z, int z_ray_stride,
+                                 const float* __restrict__ rays_d, int n_rays, int n_samples,
+                                 float* __restrict__ rgb_out, float* __restrict__ depth_out,
+                                 float* __restrict__ acc_out, float* __restrict__ weights_out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float dx = rays_d[3L * r], dy = rays_d[3L * r + 1], dz = rays_d[3L * r + 2];
+  const float norm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+  const float* zr = z + long(r) * z_ray_stride;
+  const long base = long(r) * n_samples;
+  float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, dep = 0.0f, acc = 0.0f;
+  float z_cur = zr[0];
+  for (int s = 0; s < n_samples; ++s) {
+    const float z_next = s + 1 < n_samples ? zr[s + 1] : 0.0f;
+    const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(z_next, z_cur) : 1e10f, norm);
+    const float sg = relu(sigma[(base + s) * sigma_stride]);
+    const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-sg, dist)));
+    const float w = __fmul_rn(alpha, T);
+    const float* c = rgb + (base + s) * rgb_stride;
+    cr = __fadd_rn(cr, __fmul_rn(w, c[0]));
+    cg = __fadd_rn(cg, __fmul_rn(w, c[1]));
+    cb = __fadd_rn(cb, __fmul_rn(w, c[2]));
+    dep = __fadd_rn(dep, __fmul_rn(w, z_cur));
+    acc = __fadd_rn(acc, w);
+    if (weights_out) weights_out[base + s] = w;
+    T = __fmul_rn(T, __fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f));
+    z_cur = z_next;
+  }
+  rgb_out[3L * r] = cr;
+  rgb_out[3L * r + 1] = cg;
+  rgb_out[3L * r + 2] = cb;
+  depth_out[r] = dep;
+  if (acc_out) acc_out[r] = acc;
+}
+
+// Fixed VolumeRenderer.importance_sample (rendering.py:54-100; the reference's
+// gather at :89-90 crashes): pdf = (w+1e-5)/sum, sequential sum and cumsum;
+// u ascending per ray (inverse CDF is monotone, so the importance samples come
+// out sorted and merge with the sorted coarse z in one pass).
+constexpr int kMaxCoarse = 256;
+__global__ void importance_kernel(const float* __restrict__ z_coarse, int z_ray_stride,
+                                  const float* __restrict__ weights, const float* __restrict__ u,
+                                  int u_ray_stride, int n_rays, int n_coarse, int n_importance,
+                                  float* __restrict__ z_fine) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float* zr = z_coarse + long(r) * z_ray_stride;
+  const float* wr = weights + long(r) * n_coarse;
+  const float* ur = u + long(r) * u_ray_stride;
+  float* out = z_fine + long(r) * (n_coarse + n_importance);
+  float cdf[kMaxCoarse + 1];
+  float total = 0.0f;
+  for (int i = 0; i < n_coarse; ++i) total = __fadd_rn(total, __fadd_rn(wr[i], 1e-5f));
+  cdf[0] = 0.0f;
+  for (int i = 0; i < n_coarse; ++i) cdf[i + 1] = __fadd_rn(cdf[i], __fdiv_rn(__fadd_rn(wr[i], 1e-5f), total));
+  int ic = 0;        // next coarse sample to emit
+  int o = 0;
+  int lo = 0;        // searchsorted hint: u ascending
+  for (int k = 0; k < n_importance; ++k) {
+    const float uk = ur[k];
+    // torch.searchsorted(cdf, u, right=True): count of cdf entries <= u
+    int idx = lo;
+    while (idx <= n_coarse && cdf[idx] <= uk) ++idx;
+    lo = idx;
+    const int below = min(max(idx - 1, 0), n_coarse - 1);
+    const int above = min(max(idx, 0), n_coarse - 1);
+    const float cb = cdf[below], ca = cdf[above];
+    float denom = __fsub_rn(ca, cb);
+    if (denom < 1e-5f) denom = 1.0f;
+    const float t = __fdiv_rn(__fsub_rn(uk, cb), denom);
+    const float zb = zr[below];
+    const float zs = __fadd_rn(zb, __fmul_rn(t, __fsub_rn(zr[above], zb)));
+    while (ic < n_coarse && zr[ic] <= zs) out[o++] = zr[ic++];
+    out[o++] = zs;
+  }
+  while (ic < n_coarse) out[o++] = zr[ic++];
+}
+
+}  // namespace
+
+hipError_t launch_generate_rays(const float* c2w, int width, int height, int row0, int row1, float focal,
+                                float* rays_o, float* rays_d, hipStream_t stream) {
+  Pose pose;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) pose.r[3 * i + j] = c2w[4 * i + j];
+    pose.t[i] = c2w[4 * i + 3];
+  }
+  const long n = long(row1 - row0) * width;
+  if (n <= 0) return hipSuccess;
+  const int threads = 256;
+  const dim3 grid{unsigned((n + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  // `width * 0.5` / `height * 0.5` are exact in fp32 for any image size we accept
+  hipLaunchKernelGGL(rays_kernel, grid, block, 0, stream, pose, width, float(width) * 0.5f, float(height) * 0.5f,
+                     focal, row0, n, rays_o, rays_d);
+  return hipGetLastError();
+}
+
+hipError_t launch_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride, const float* z,
+                            int z_ray_stride, const float* rays_d, int n_rays, int n_samples, float* rgb_out,
+                            float* depth_out, float* acc_out, float* weights_out, hipStream_t stream) {
+  if (n_rays <= 0) return hipSuccess;
+  const int threads = 128;
+  const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  hipLaunchKernelGGL(composite_kernel, grid, block, 0, stream, sigma, sigma_stride, rgb, rgb_stride, z, z_ray_stride,
+                     rays_d, n_rays, n_samples, rgb_out, depth_out, acc_out, weights_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_importance(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
+                             int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine,
+                             hipStream_t stream) {
+  if (n_rays <= 0) return hipSuccess;
+  if (n_coarse > kMaxCoarse) return hipErrorInvalidValue;
+  const int threads = 64;
+  const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  hipLaunchKernelGGL(importance_kernel, grid, block, 0, stream, z_coarse, z_ray_stride, weights, u, u_ray_stride,
+                     n_rays, n_coarse, n_importance, z_fine);
+  return hipGetLastError();
+}
+
+}  // namespace nerf

@@ -1,0 +1,226 @@
+"""ctypes binding of libnerf_mi355x.so (C ABI: include/nerf_mi355x.h).
+
+The library is built in-tree (``nerf-dbr_amd/csrc/Makefile`` ->
+``nerf_amd/_lib/libnerf_mi355x.so``).  There is no CPU or PyTorch fallback:
+if the library is missing or no gfx950 device is present, constructing a
+``Device`` raises ``RuntimeError`` (the exception type the reference's suite
+probes renderers with, ``src/benchmark/benchmark_suite.py:80-92``).
+
+Tensors cross the boundary as raw device pointers (``tensor.data_ptr()``) and
+the HIP stream as ``torch.cuda.current_stream().cuda_stream``; PyTorch is only
+the device-memory and stream plumbing here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Mapping, Optional, Sequence
+
+import numpy as np
+
+from .weights import LAYER_SPECS, validate_state_dict
+
+LIB_NAME = "libnerf_mi355x.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", LIB_NAME)
+
+NERF_OK = 0
+NERF_FP32, NERF_BF16 = 0, 1
+NERF_NET_COARSE, NERF_NET_FINE = 0, 1
+NERF_N_PARAMS = 22
+NERF_N_STAGES = 5
+STAGES = ("rays", "coarse_mlp", "importance", "fine_mlp", "composite")
+
+PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16}
+
+# Every symbol include/nerf_mi355x.h declares, with its ctypes signature.
+_c = ctypes
+_P = _c.c_void_p
+_FP = _c.POINTER(_c.c_float)
+SIGNATURES = {
+    "nerf_abi_version": (_c.c_int, []),
+    "nerf_last_error": (_c.c_char_p, []),
+    "nerf_ctx_create": (_c.c_int, [_c.c_int, _c.POINTER(_P)]),
+    "nerf_ctx_destroy": (None, [_P]),
+    "nerf_device_name": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_int]),
+    "nerf_ctx_load_weights": (_c.c_int, [_P, _c.c_int, _c.POINTER(_FP), _c.c_int]),
+    "nerf_packed_sizes": (None, [_c.POINTER(_c.c_size_t)] * 3),
+    "nerf_pack_weights": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P, _P, _P]),
+    "nerf_uniform_z": (None, [_FP, _c.c_int, _c.c_float, _c.c_float, _FP]),
+    "nerf_generate_rays": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _P, _P, _P]),
+    "nerf_mlp_forward": (_c.c_int, [_P, _c.c_int, _c.c_int, _P, _P, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P]),
+    "nerf_query": (_c.c_int, [_P, _c.c_int, _c.c_int, _P, _P, _c.c_int, _P, _P]),
+    "nerf_composite": (_c.c_int, [_P, _c.c_int, _P, _c.c_int, _P, _c.c_int, _P, _c.c_int, _c.c_int,
+                                  _P, _P, _P, _P, _P]),
+    "nerf_importance_sample": (_c.c_int, [_P, _c.c_int, _P, _P, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P]),
+    "nerf_render": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float,
+                               _c.c_float, _FP, _c.c_int, _c.c_int, _FP, _c.c_int, _P, _P, _P]),
+    "nerf_ctx_set_profiling": (_c.c_int, [_P, _c.c_int]),
+    "nerf_ctx_stage_ms": (_c.c_int, [_P, _FP]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NerfError(RuntimeError):
+    pass
+
+
+def library_path() -> str:
+    return os.environ.get("NERF_MI355X_LIB", LIB_PATH)
+
+
+def load_library() -> ctypes.CDLL:
+    """Load and type the shared library (no device needed).  RuntimeError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not os.path.exists(path):
+        raise NerfError(f"{LIB_NAME} not built at {path}; run `make -C nerf-dbr_amd/csrc` "
+                        f"or __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != NERF_OK:
+        msg = load_library().nerf_last_error().decode(errors="replace")
+        raise NerfError(f"libnerf_mi355x error {rc}: {msg}")
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(_FP)
+
+
+def _param_list(sd: Mapping[str, np.ndarray]):
+    validate_state_dict(sd)
+    arrs = []
+    for name, _, _ in LAYER_SPECS:
+        for suffix in ("weight", "bias"):
+            arrs.append(np.ascontiguousarray(sd[f"{name}.{suffix}"], dtype=np.float32))
+    ptrs = (_FP * NERF_N_PARAMS)(*[_fptr(a) for a in arrs])
+    return arrs, ptrs
+
+
+def pack_weights(sd: Mapping[str, np.ndarray]):
+    """Host-only packing (the same code the loader runs): (f32 blob, bf16 blob as uint16, params)."""
+    lib = load_library()
+    sizes = [ctypes.c_size_t() for _ in range(3)]
+    lib.nerf_packed_sizes(*[ctypes.byref(s) for s in sizes])
+    f32 = np.zeros(sizes[0].value // 4, np.float32)
+    bf = np.zeros(sizes[1].value // 2, np.uint16)
+    prm = np.zeros(sizes[2].value // 4, np.float32)
+    keep, ptrs = _param_list(sd)
+    _check(lib.nerf_pack_weights(ptrs, NERF_N_PARAMS, f32.ctypes.data_as(_P), bf.ctypes.data_as(_P),
+                                 prm.ctypes.data_as(_P)))
+    del keep
+    return f32, bf, prm
+
+
+def uniform_z(t_vals: np.ndarray, near: float, far: float) -> np.ndarray:
+    lib = load_library()
+    t = np.ascontiguousarray(t_vals, dtype=np.float32)
+    z = np.empty_like(t)
+    lib.nerf_uniform_z(_fptr(t), t.size, near, far, _fptr(z))
+    return z
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _stream(stream) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+class Device:
+    """One library context on one GPU (weights resident, scratch reused)."""
+
+    def __init__(self, device_index: int = 0):
+        lib = load_library()
+        self.lib = lib
+        self.index = device_index
+        ctx = ctypes.c_void_p()
+        _check(lib.nerf_ctx_create(device_index, ctypes.byref(ctx)))
+        self._ctx = ctx
+        self.loaded = set()
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self.lib.nerf_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def name(self) -> str:
+        buf = ctypes.create_string_buffer(256)
+        _check(self.lib.nerf_device_name(self.index, buf, 256))
+        return buf.value.decode()
+
+    def load_weights(self, net: int, sd: Mapping[str, np.ndarray]) -> None:
+        keep, ptrs = _param_list(sd)
+        _check(self.lib.nerf_ctx_load_weights(self._ctx, net, ptrs, NERF_N_PARAMS))
+        del keep
+        self.loaded.add(net)
+
+    # ---- granular device calls (torch CUDA tensors in, results written in place) ----
+    def generate_rays(self, c2w: np.ndarray, width: int, height: int, row0: int, row1: int, focal: float,
+                      rays_o, rays_d, stream=None) -> None:
+        pose = np.ascontiguousarray(np.asarray(c2w, dtype=np.float32).reshape(4, 4))
+        _check(self.lib.nerf_generate_rays(self._ctx, _fptr(pose), width, height, row0, row1, focal,
+                                           _ptr(rays_o), _ptr(rays_d), _stream(stream)))
+
+    def mlp_forward(self, net: int, precision: int, rays_o, rays_d, z, z_ray_stride: int, n_rays: int,
+                    n_samples: int, out, stream=None) -> None:
+        _check(self.lib.nerf_mlp_forward(self._ctx, net, precision, _ptr(rays_o), _ptr(rays_d), _ptr(z),
+                                         z_ray_stride, n_rays, n_samples, _ptr(out), _stream(stream)))
+
+    def query(self, net: int, precision: int, positions, directions, out, stream=None) -> None:
+        _check(self.lib.nerf_query(self._ctx, net, precision, _ptr(positions), _ptr(directions),
+                                   positions.shape[0], _ptr(out), _stream(stream)))
+
+    def composite(self, sigma, sigma_stride: int, rgb, rgb_stride: int, z, z_ray_stride: int, rays_d,
+                  n_rays: int, n_samples: int, rgb_out, depth_out, acc_out=None, weights_out=None,
+                  stream=None) -> None:
+        _check(self.lib.nerf_composite(_ptr(sigma), sigma_stride, _ptr(rgb), rgb_stride, _ptr(z), z_ray_stride,
+                                       _ptr(rays_d), n_rays, n_samples, _ptr(rgb_out), _ptr(depth_out),
+                                       _ptr(acc_out), _ptr(weights_out), _stream(stream)))
+
+    def importance_sample(self, z_coarse, z_ray_stride: int, weights, u, u_ray_stride: int, n_rays: int,
+                          n_coarse: int, n_importance: int, z_fine, stream=None) -> None:
+        _check(self.lib.nerf_importance_sample(_ptr(z_coarse), z_ray_stride, _ptr(weights), _ptr(u), u_ray_stride,
+                                               n_rays, n_coarse, n_importance, _ptr(z_fine), _stream(stream)))
+
+    def render(self, c2w: np.ndarray, width: int, height: int, row0: int, row1: int, focal: float, near: float,
+               far: float, t_vals: np.ndarray, n_importance: int, u: Optional[np.ndarray], precision: int,
+               rgb_out, depth_out, stream=None) -> None:
+        pose = np.ascontiguousarray(np.asarray(c2w, dtype=np.float32).reshape(4, 4))
+        t = np.ascontiguousarray(t_vals, dtype=np.float32)
+        uu = None if u is None else np.ascontiguousarray(u, dtype=np.float32)
+        _check(self.lib.nerf_render(self._ctx, _fptr(pose), width, height, row0, row1, focal, near, far, _fptr(t),
+                                    t.size, n_importance, None if uu is None else _fptr(uu), precision,
+                                    _ptr(rgb_out), _ptr(depth_out), _stream(stream)))
+
+    def set_profiling(self, enable: bool) -> None:
+        _check(self.lib.nerf_ctx_set_profiling(self._ctx, 1 if enable else 0))
+
+    def stage_ms(self) -> dict:
+        ms = (ctypes.c_float * NERF_N_STAGES)()
+        _check(self.lib.nerf_ctx_stage_ms(self._ctx, ms))
+        return dict(zip(STAGES, [float(v) for v in ms]))
+
+
+def exported_symbols() -> Sequence[str]:
+    return tuple(SIGNATURES)

@@ -1,0 +1,151 @@
+"""NeRF weight schema, checkpoint I/O and the deterministic synthetic checkpoint.
+
+The network is the reference's ``NeRFModel`` (``src/models/nerf.py:48-131``):
+eight 256-wide trunk layers with the positional encoding re-injected before
+layer 4 (``nerf.py:107-110``), a 1-wide density head (``nerf.py:84,114``) and a
+two-layer colour head fed with ``[x, PE4(d)]`` (``nerf.py:87-90,117-129``).
+Weights are stored exactly as ``nn.Linear`` stores them: ``weight`` is
+``[out, in]`` row-major fp32, ``bias`` is ``[out]``.
+
+Checkpoints use the reference trainer's dict layout
+(``src/training/trainer.py:376-384``): ``{'coarse_model': state_dict,
+'fine_model': state_dict, ...}``; renderers only read the two model entries
+(``src/benchmark/base_renderer.py:42-48``).  Unlike the reference
+(``base_renderer.py:42``, ``weights_only=False``) checkpoints are loaded with
+``torch.load(weights_only=True)``: nothing in a checkpoint file is executed.
+
+No trained checkpoint in this layout exists, and a randomly
+initialised net renders an all-black image.  ``synthetic_state_dict`` builds a
+*conditioned* random net instead: ``nn.Linear``'s default
+init distribution (U(-1/sqrt(fan_in), 1/sqrt(fan_in)) for weight and bias) drawn
+from numpy's legacy ``RandomState`` (a stream numpy keeps stable across
+releases), then trunk weights x2, density weight x30, density bias = 0.2 and
+the last colour weight x8, so images have real structure and depth.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+from typing import Dict, List, Mapping, Tuple
+
+import numpy as np
+
+POS_L = 10            # nerf.py:50 (pos_L default)
+DIR_L = 4             # nerf.py:50 (dir_L default)
+HIDDEN = 256          # nerf.py:50 (hidden_dim default)
+POS_DIM = 3 + 3 * 2 * POS_L   # 63 (nerf.py:64 comment says 60; it is 63)
+DIR_DIM = 3 + 3 * 2 * DIR_L   # 27
+SKIP_LAYER = 4                # nerf.py:108 (`if i == 4`)
+
+# (state-dict prefix, out_features, in_features) in forward order (nerf.py:72-90)
+LAYER_SPECS: List[Tuple[str, int, int]] = (
+    [("layers.0", HIDDEN, POS_DIM)]
+    + [(f"layers.{i}", HIDDEN, HIDDEN) for i in (1, 2, 3)]
+    + [("layers.4", HIDDEN, HIDDEN + POS_DIM)]
+    + [(f"layers.{i}", HIDDEN, HIDDEN) for i in (5, 6, 7)]
+    + [("density_head", 1, HIDDEN),
+       ("color_layers.0", HIDDEN // 2, HIDDEN + DIR_DIM),
+       ("color_layers.1", 3, HIDDEN // 2)]
+)
+
+N_PARAMS = sum(o * i + o for _, o, i in LAYER_SPECS)          # 530,052
+# multiply-accumulates per sample: every Linear, unpadded
+MACS_PER_SAMPLE = sum(o * i for _, o, i in LAYER_SPECS)       # 527,872
+FLOPS_PER_SAMPLE = 2 * MACS_PER_SAMPLE                        # 1,055,744
+
+StateDict = Dict[str, np.ndarray]
+
+
+def expected_shapes() -> Dict[str, Tuple[int, ...]]:
+    out: Dict[str, Tuple[int, ...]] = {}
+    for name, o, i in LAYER_SPECS:
+        out[f"{name}.weight"] = (o, i)
+        out[f"{name}.bias"] = (o,)
+    return out
+
+
+def validate_state_dict(sd: Mapping[str, np.ndarray]) -> None:
+    """Strict key/shape check, the same contract as ``load_state_dict(strict=True)``."""
+    exp = expected_shapes()
+    missing = sorted(set(exp) - set(sd))
+    unexpected = sorted(set(sd) - set(exp))
+    if missing or unexpected:
+        raise KeyError(f"state_dict mismatch: missing={missing} unexpected={unexpected}")
+    for k, shape in exp.items():
+        if tuple(sd[k].shape) != shape:
+            raise ValueError(f"state_dict[{k!r}] has shape {tuple(sd[k].shape)}, expected {shape}")
+
+
+def synthetic_state_dict(seed: int, conditioned: bool = True) -> StateDict:
+    """Deterministic NeRFModel weights (see module docstring)."""
+    rng = np.random.RandomState(seed)
+    sd: StateDict = {}
+    for name, o, i in LAYER_SPECS:
+        bound = 1.0 / np.sqrt(i)
+        sd[f"{name}.weight"] = rng.uniform(-bound, bound, size=(o, i)).astype(np.float32)
+        sd[f"{name}.bias"] = rng.uniform(-bound, bound, size=(o,)).astype(np.float32)
+    if conditioned:
+        for li in range(8):
+            sd[f"layers.{li}.weight"] *= np.float32(2.0)
+        sd["density_head.weight"] *= np.float32(30.0)
+        sd["density_head.bias"][:] = np.float32(0.2)
+        sd["color_layers.1.weight"] *= np.float32(8.0)
+    return sd
+
+
+def synthetic_models(seed: int = 0, conditioned: bool = True) -> Tuple[StateDict, StateDict]:
+    """(coarse, fine) state dicts: coarse from ``seed``, fine from ``seed + 1``."""
+    return synthetic_state_dict(seed, conditioned), synthetic_state_dict(seed + 1, conditioned)
+
+
+def state_dict_digest(sd: Mapping[str, np.ndarray]) -> str:
+    h = hashlib.sha256()
+    for name, _, _ in LAYER_SPECS:
+        for suffix in ("weight", "bias"):
+            h.update(np.ascontiguousarray(sd[f"{name}.{suffix}"], dtype=np.float32).tobytes())
+    return h.hexdigest()
+
+
+def _to_numpy(sd) -> StateDict:
+    out: StateDict = {}
+    for k, v in sd.items():
+        if hasattr(v, "detach"):
+            v = v.detach().cpu().numpy()
+        out[k] = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+    return out
+
+
+def save_checkpoint(path: str, coarse: Mapping[str, np.ndarray], fine: Mapping[str, np.ndarray]) -> str:
+    """Write a reference-format checkpoint (``trainer.py:376-384``, model entries only)."""
+    import torch
+
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    ckpt = {
+        "coarse_model": {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in coarse.items()},
+        "fine_model": {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in fine.items()},
+    }
+    torch.save(ckpt, path)
+    return path
+
+
+def load_checkpoint(path: str) -> Tuple[StateDict, StateDict]:
+    """Load ``(coarse, fine)`` from a reference-format checkpoint.
+
+    Raises ``FileNotFoundError`` when the file is missing: unlike the reference
+    (``base_renderer.py:62-76``) there is no silent random-weight fallback.
+    """
+    import torch
+
+    if not os.path.exists(path):
+        raise FileNotFoundError(path)
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    coarse, fine = _to_numpy(ckpt["coarse_model"]), _to_numpy(ckpt["fine_model"])
+    validate_state_dict(coarse)
+    validate_state_dict(fine)
+    return coarse, fine
+
+
+def write_synthetic_checkpoint(path: str, seed: int = 0) -> str:
+    coarse, fine = synthetic_models(seed)
+    return save_checkpoint(path, coarse, fine)

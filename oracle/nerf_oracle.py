@@ -1,0 +1,237 @@
+"""ORACLE -- test infrastructure, not product code.
+
+A CPU (PyTorch fp32) restatement of the reference's NeRF render path, written
+from the semantics in SURVEY §8a.  It is the parity checker for the HIP path and
+the timed ``cpu_baseline`` in ``bench.py``.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg import it; the
+product package (``nerf-dbr_amd/nerf_amd``) never does and has no CPU fallback.
+
+Pinning: every function below is checked against golden vectors produced by the
+reference itself (``tests/golden/make_golden.py``; ``tests/test_oracle_golden.py``):
+rays, t/z tables and stratified samples bit-exactly, positional encoding,
+network outputs, compositing and full ``render_image`` images at fp32 rounding.
+
+The hierarchical sampler is the one piece with no working reference: the
+reference's ``VolumeRenderer.importance_sample`` (``src/utils/rendering.py:54-100``)
+crashes at its gather (``:89-90``) and nothing calls it.  Here it is
+restated with the gather fixed as SURVEY §8a-H prescribes, and two definitions
+the build makes (documented in DESIGN.md): the pdf normaliser is the
+*sequential* sum (the last element of the cumsum) so it is bitwise reproducible
+on any host, and the fine set is the sorted union of coarse and importance
+samples.  Its tests are "parity unpinned" beyond those pieces.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Mapping, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+NEAR, FAR, FOCAL = 2.0, 6.0, 800.0      # base_renderer.py:109-110, :224
+CHUNK = 512                              # pytorch_renderers.py:137
+
+
+def _t(x) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.detach().to("cpu", torch.float32)
+    return torch.as_tensor(np.asarray(x, dtype=np.float32))
+
+
+class Net:
+    """fp32 weights of one NeRFModel as CPU tensors (layout: nn.Linear [out, in])."""
+
+    def __init__(self, sd: Mapping[str, np.ndarray]):
+        self.p: Dict[str, torch.Tensor] = {k: _t(v).contiguous() for k, v in sd.items()}
+
+    def lin(self, name: str, x: torch.Tensor) -> torch.Tensor:
+        return F.linear(x, self.p[f"{name}.weight"], self.p[f"{name}.bias"])
+
+
+# ---------------------------------------------------------------- a1 rays --
+def generate_rays(c2w, width: int, height: int, focal: float = FOCAL):
+    """base_renderer.py:223-258: pixel corners, dir=((i-W/2)/f, -(j-H/2)/f, -1), R·dir."""
+    c2w = _t(c2w)
+    i = torch.linspace(0, width - 1, width)[None, :].expand(height, width)
+    j = torch.linspace(0, height - 1, height)[:, None].expand(height, width)
+    dirs = torch.stack([(i - width * 0.5) / focal, -(j - height * 0.5) / focal, -torch.ones_like(i)], -1)
+    rot = c2w[:3, :3]
+    # sum over the 3 products, accumulated in order (x, y, z): ((p0 + p1) + p2)
+    prod = dirs[..., None, :] * rot
+    rays_d = (prod[..., 0] + prod[..., 1]) + prod[..., 2]
+    rays_o = c2w[:3, 3].expand(rays_d.shape)
+    return rays_o, rays_d
+
+
+# ------------------------------------------------------------ a2 sampling --
+def t_vals(n_samples: int) -> torch.Tensor:
+    return torch.linspace(0.0, 1.0, n_samples)
+
+
+def uniform_z(n_samples: int, near: float = NEAR, far: float = FAR) -> torch.Tensor:
+    """base_renderer.py:274-275: z = near*(1-t) + far*t (fp32, this op order)."""
+    t = t_vals(n_samples)
+    return near * (1.0 - t) + far * t
+
+
+def stratified_z(z: torch.Tensor, t_rand: torch.Tensor) -> torch.Tensor:
+    """rendering.py:42-47 with the uniform draw injected: lower + (upper-lower)*t_rand."""
+    z = _t(z)
+    t_rand = _t(t_rand)
+    z = z.expand(t_rand.shape)
+    mids = 0.5 * (z[..., 1:] + z[..., :-1])
+    upper = torch.cat([mids, z[..., -1:]], -1)
+    lower = torch.cat([z[..., :1], mids], -1)
+    return lower + (upper - lower) * t_rand
+
+
+def sample_points(rays_o: torch.Tensor, rays_d: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
+    """base_renderer.py:279: o + d*z, a multiply then an add (no fused multiply-add)."""
+    return rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
+
+
+# ------------------------------------------------------------ a3 encoding --
+def positional_encoding(x: torch.Tensor, n_freqs: int) -> torch.Tensor:
+    """nerf.py:16-45: [x, sin(2^k*pi*x), cos(2^k*pi*x) for k < L] (fp32 argument)."""
+    x = _t(x)
+    out = [x]
+    for k in range(n_freqs):
+        c = torch.tensor(2.0 ** k, dtype=torch.float32) * math.pi    # fl(2^k * pi), exact scaling
+        arg = c * x
+        out.append(torch.sin(arg))
+        out.append(torch.cos(arg))
+    return torch.cat(out, -1)
+
+
+# ----------------------------------------------------------------- a4 MLP --
+def nerf_forward(net: Net, positions: torch.Tensor, directions: Optional[torch.Tensor]):
+    """nerf.py:92-131: 8x(Linear+ReLU) with PE re-injected before layer 4, heads."""
+    pe = positional_encoding(positions, 10)
+    x = pe
+    for i in range(8):
+        if i == 4:
+            x = torch.cat([x, pe], -1)          # hidden first, then pe (nerf.py:109-110)
+        x = F.relu(net.lin(f"layers.{i}", x))
+    sigma = F.relu(net.lin("density_head", x))
+    h = torch.cat([x, positional_encoding(directions, 4)], -1) if directions is not None else x
+    h = F.relu(net.lin("color_layers.0", h))
+    rgb = torch.sigmoid(net.lin("color_layers.1", h))
+    return sigma, rgb
+
+
+# ----------------------------------------------------------- a6 composite --
+def composite(sigma: torch.Tensor, rgb: torch.Tensor, z: torch.Tensor, rays_d: torch.Tensor,
+              with_weights: bool = False):
+    """pytorch_renderers.py:105-125 (== rendering.py:102-143 plus acc/weights)."""
+    sigma, rgb, z, rays_d = _t(sigma), _t(rgb), _t(z), _t(rays_d)
+    dists = z[..., 1:] - z[..., :-1]
+    dists = torch.cat([dists, torch.full_like(dists[..., :1], 1e10)], -1)
+    dists = dists * torch.norm(rays_d[..., None, :], dim=-1)
+    alpha = 1.0 - torch.exp(-F.relu(sigma[..., 0]) * dists)
+    trans = torch.cumprod(1.0 - alpha + 1e-10, -1)
+    trans = torch.cat([torch.ones_like(trans[..., :1]), trans[..., :-1]], -1)
+    weights = alpha * trans
+    rgb_map = torch.sum(weights[..., None] * rgb, -2)
+    depth_map = torch.sum(weights * z, -1)
+    if with_weights:
+        return rgb_map, depth_map, torch.sum(weights, -1), weights
+    return rgb_map, depth_map
+
+
+# ------------------------------------------------- a8-H importance sample --
+def importance_sample(z: torch.Tensor, weights: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """rendering.py:72-95 with the gather fixed, sequential normaliser."""
+    z, weights, u = _t(z), _t(weights), _t(u)
+    n = z.shape[-1]
+    w = weights + 1e-5
+    total = torch.cumsum(w, -1)[..., -1:]
+    pdf = w / total
+    cdf = torch.cumsum(pdf, -1)
+    cdf = torch.cat([torch.zeros_like(cdf[..., :1]), cdf], -1)
+    idx = torch.searchsorted(cdf.contiguous(), u.contiguous(), right=True)
+    below = torch.clamp(idx - 1, 0, n - 1)
+    above = torch.clamp(idx, 0, n - 1)
+    cdf_b, cdf_a = torch.gather(cdf, -1, below), torch.gather(cdf, -1, above)
+    z_b, z_a = torch.gather(z, -1, below), torch.gather(z, -1, above)
+    denom = cdf_a - cdf_b
+    denom = torch.where(denom < 1e-5, torch.ones_like(denom), denom)
+    t = (u - cdf_b) / denom
+    return z_b + t * (z_a - z_b)
+
+
+def fine_z(z_coarse: torch.Tensor, weights: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    z_imp = importance_sample(z_coarse, weights, u)
+    return torch.sort(torch.cat([_t(z_coarse), z_imp], -1), -1).values
+
+
+def default_u(n_rays: int, n_importance: int) -> torch.Tensor:
+    """Deterministic benchmark draw: u = linspace(0, 1, n_importance) for every ray."""
+    return torch.linspace(0.0, 1.0, n_importance).expand(n_rays, n_importance)
+
+
+# ---------------------------------------------------------- a7 full image --
+def render_rays(net: Net, rays_o, rays_d, n_samples: int, chunk: int = CHUNK,
+                near: float = NEAR, far: float = FAR):
+    """_render_ray_chunk (pytorch_renderers.py:156-170) over 512-ray chunks."""
+    rays_o, rays_d = _t(rays_o).reshape(-1, 3), _t(rays_d).reshape(-1, 3)
+    z_row = uniform_z(n_samples, near, far)
+    rgbs, depths = [], []
+    with torch.no_grad():
+        for c in range(0, rays_o.shape[0], chunk):
+            o, d = rays_o[c:c + chunk], rays_d[c:c + chunk]
+            z = z_row.expand(o.shape[0], n_samples)
+            pts = sample_points(o, d, z)
+            dirs = d[:, None, :].expand_as(pts).reshape(-1, 3)
+            sigma, rgb = nerf_forward(net, pts.reshape(-1, 3), dirs)
+            r, dep = composite(sigma.reshape(*pts.shape[:-1], 1), rgb.reshape(pts.shape), z, d)
+            rgbs.append(r)
+            depths.append(dep)
+    if not rgbs:
+        return torch.zeros(0, 3), torch.zeros(0)
+    return torch.cat(rgbs), torch.cat(depths)
+
+
+def render_image(net: Net, c2w, resolution: Tuple[int, int], n_samples: int = 64,
+                 rows: Optional[Tuple[int, int]] = None):
+    """PyTorchCPURenderer.render_image (pytorch_renderers.py:127-154); optional row band."""
+    width, height = resolution
+    rays_o, rays_d = generate_rays(c2w, width, height)
+    r0, r1 = rows if rows is not None else (0, height)
+    rgb, depth = render_rays(net, rays_o[r0:r1], rays_d[r0:r1], n_samples)
+    return rgb.reshape(r1 - r0, width, 3), depth.reshape(r1 - r0, width)
+
+
+def render_image_hierarchical(coarse: Net, fine: Net, c2w, resolution: Tuple[int, int],
+                              n_coarse: int = 64, n_importance: int = 128,
+                              u: Optional[torch.Tensor] = None, chunk: int = CHUNK,
+                              rows: Optional[Tuple[int, int]] = None):
+    """Build-defined 64+128 hierarchical render: coarse net on the
+    uniform samples, importance samples from its weights, fine net on the sorted union."""
+    width, height = resolution
+    rays_o, rays_d = generate_rays(c2w, width, height)
+    r0, r1 = rows if rows is not None else (0, height)
+    rays_o, rays_d = rays_o[r0:r1].reshape(-1, 3), rays_d[r0:r1].reshape(-1, 3)
+    n = rays_o.shape[0]
+    if u is None:
+        u = default_u(n, n_importance)
+    u = _t(u)
+    z_row = uniform_z(n_coarse)
+    rgbs, depths = [], []
+    with torch.no_grad():
+        for c in range(0, n, chunk):
+            o, d = rays_o[c:c + chunk], rays_d[c:c + chunk]
+            m = o.shape[0]
+            zc = z_row.expand(m, n_coarse)
+            pts = sample_points(o, d, zc)
+            dirs = d[:, None, :].expand_as(pts).reshape(-1, 3)
+            s, r = nerf_forward(coarse, pts.reshape(-1, 3), dirs)
+            _, _, _, w = composite(s.reshape(m, n_coarse, 1), r.reshape(m, n_coarse, 3), zc, d, True)
+            zf = fine_z(zc, w, u[c:c + chunk])
+            pts = sample_points(o, d, zf)
+            dirs = d[:, None, :].expand_as(pts).reshape(-1, 3)
+            s, r = nerf_forward(fine, pts.reshape(-1, 3), dirs)
+            rr, dd = composite(s.reshape(m, -1, 1), r.reshape(m, -1, 3), zf, d)
+            rgbs.append(rr)
+            depths.append(dd)
+    return torch.cat(rgbs).reshape(r1 - r0, width, 3), torch.cat(depths).reshape(r1 - r0, width)

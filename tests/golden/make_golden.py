@@ -1,0 +1,249 @@
+"""Generate the golden vectors in tests/golden/ from the reference itself.
+
+Run in the development container only (the reference is not on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+It imports the reference's Python renderer, model and volume-render utilities
+(bypassing ``src/benchmark/__init__.py``, whose ``numba`` import is absent here
+-- SURVEY §8c import recipe), feeds them the deterministic synthetic checkpoint
+of ``nerf_amd.weights`` and records inputs and outputs as ``.npz`` data.  Only
+data is committed; no reference source is copied.
+
+Fixtures (every array fp32 unless noted):
+  rays.npz        generate_rays        base_renderer.py:223-258
+  tvals.npz       sample_points_on_rays base_renderer.py:260-281 (z only)
+  pe.npz          PositionalEncoding.encode nerf.py:24-45, L=10 and L=4
+  mlp.npz         NeRFModel.forward    nerf.py:92-131 (coarse and fine)
+  composite.npz   execute_volume_rendering pytorch_renderers.py:105-125 and
+                  VolumeRenderer.volume_render rendering.py:102-143
+  stratified.npz  VolumeRenderer.sample_points_on_rays(perturb=True) rendering.py:17-52
+  render_*.npz    PyTorchCPURenderer.render_image pytorch_renderers.py:127-170
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+import time
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "nerf-dbr_amd"))
+
+from nerf_amd import weights as W  # noqa: E402
+
+
+def import_reference(ref_root: str):
+    sys.path.insert(0, ref_root)
+    import src  # noqa: F401
+
+    bp = types.ModuleType("src.benchmark")
+    bp.__path__ = [os.path.join(ref_root, "src", "benchmark")]
+    sys.modules["src.benchmark"] = bp
+    from src.benchmark.pytorch_renderers import PyTorchCPURenderer
+    from src.models.nerf import NeRFModel, PositionalEncoding
+    from src.utils.rendering import VolumeRenderer
+
+    return PyTorchCPURenderer, NeRFModel, PositionalEncoding, VolumeRenderer
+
+
+def suite_poses(n_views: int = 2):
+    """Same construction as benchmark_suite.py:132-149 (data, not imported)."""
+    import torch
+
+    poses = []
+    for i in range(n_views):
+        a = i * 2 * np.pi / n_views
+        c2w = torch.eye(4, dtype=torch.float32)
+        c2w[0, 0] = np.cos(a)
+        c2w[0, 2] = np.sin(a)
+        c2w[2, 0] = -np.sin(a)
+        c2w[2, 2] = np.cos(a)
+        c2w[2, 3] = 4.0
+        poses.append(c2w)
+    return poses
+
+
+def off_axis_pose():
+    """A look-at pose that is not axis-aligned (exercises every rotation term)."""
+    import torch
+
+    eye = np.array([2.7, 1.9, 2.3], dtype=np.float64)
+    fwd = -eye / np.linalg.norm(eye)
+    up = np.array([0.0, 1.0, 0.0])
+    right = np.cross(fwd, up)
+    right /= np.linalg.norm(right)
+    up2 = np.cross(right, fwd)
+    c2w = np.eye(4)
+    c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = right, up2, -fwd, eye
+    return torch.tensor(c2w, dtype=torch.float32)
+
+
+def main(ref_root: str = "/root/reference") -> None:
+    import torch
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    PyTorchCPURenderer, NeRFModel, PositionalEncoding, VolumeRenderer = import_reference(ref_root)
+
+    coarse_sd, fine_sd = W.synthetic_models(0)
+    ckpt_path = os.path.join(tempfile.mkdtemp(prefix="nerf_golden_"), "synthetic.pth")
+    W.save_checkpoint(ckpt_path, coarse_sd, fine_sd)
+
+    def net(sd):
+        m = NeRFModel()
+        m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in sd.items()})
+        return m.eval()
+
+    coarse, fine = net(coarse_sd), net(fine_sd)
+    renderer = PyTorchCPURenderer()
+    renderer.setup(ckpt_path)
+    poses = suite_poses(2) + [off_axis_pose()]
+    pose_arr = np.stack([p.numpy() for p in poses])
+    meta = {
+        "torch": torch.__version__,
+        "numpy": np.__version__,
+        "coarse_digest": W.state_dict_digest(coarse_sd),
+        "fine_digest": W.state_dict_digest(fine_sd),
+        "seed": 0,
+        "poses": "suite views 0,1 (benchmark_suite.py:132-149) + off-axis look-at",
+    }
+    save = lambda name, **kw: np.savez_compressed(os.path.join(HERE, name), **kw)  # noqa: E731
+
+    # ---- rays -------------------------------------------------------------
+    rays = {"poses": pose_arr}
+    for (w, h) in [(64, 48), (37, 23), (200, 150)]:
+        for pi, p in enumerate(poses):
+            ro, rd = renderer.generate_rays(p, w, h)
+            rays[f"o_{w}x{h}_{pi}"] = ro.numpy()
+            rays[f"d_{w}x{h}_{pi}"] = rd.numpy()
+    save("rays.npz", **rays)
+
+    # ---- t_vals / z_vals ----------------------------------------------------
+    tv = {}
+    ro = torch.zeros(1, 3)
+    rd = torch.ones(1, 3)
+    for s in [1, 2, 3, 16, 32, 64, 128, 192, 256]:
+        _, z = renderer.sample_points_on_rays(ro, rd, s)
+        tv[f"z_{s}"] = z[0].numpy()
+        tv[f"t_{s}"] = torch.linspace(0.0, 1.0, s).numpy()
+    save("tvals.npz", **tv)
+
+    # ---- positional encoding -----------------------------------------------
+    g = torch.Generator().manual_seed(1234)
+    x = torch.cat([
+        (torch.rand(2048, 3, generator=g) * 2 - 1) * 2.0,
+        (torch.rand(1024, 3, generator=g) * 2 - 1) * 10.5,     # suite view 1 reaches |z|~10
+        torch.tensor([[0.0, -0.0, 1.0], [10.0, -10.0, 7.25], [1e-8, -3e-39, 2.5]]),
+    ])
+    pe10 = PositionalEncoding(10).encode(x)
+    pe4 = PositionalEncoding(4).encode(x)
+    save("pe.npz", x=x.numpy(), pe10=pe10.numpy(), pe4=pe4.numpy())
+
+    # ---- MLP forward (points taken from real rays of both views) -------------
+    ro0, rd0 = renderer.generate_rays(poses[0], 64, 48)
+    ro1, rd1 = renderer.generate_rays(poses[2], 64, 48)
+    pts0, _ = renderer.sample_points_on_rays(ro0.reshape(-1, 3)[:64], rd0.reshape(-1, 3)[:64], 32)
+    pts1, _ = renderer.sample_points_on_rays(ro1.reshape(-1, 3)[-64:], rd1.reshape(-1, 3)[-64:], 32)
+    pos = torch.cat([pts0.reshape(-1, 3), pts1.reshape(-1, 3)])
+    dirs = torch.cat([rd0.reshape(-1, 3)[:64].repeat_interleave(32, 0),
+                      rd1.reshape(-1, 3)[-64:].repeat_interleave(32, 0)])
+    with torch.no_grad():
+        sf, cf = fine(pos, dirs)
+        sc, cc = coarse(pos, dirs)
+    save("mlp.npz", pos=pos.numpy(), dirs=dirs.numpy(), sigma_fine=sf.numpy(), rgb_fine=cf.numpy(),
+         sigma_coarse=sc.numpy(), rgb_coarse=cc.numpy())
+
+    # ---- compositing ---------------------------------------------------------
+    vr = VolumeRenderer("cpu")
+    comp = {}
+    g = torch.Generator().manual_seed(99)
+    cases = {}
+    for s in [16, 32, 64, 128]:
+        n = 96
+        sig = torch.rand(n, s, 1, generator=g) * 3.0 - 0.5          # includes negatives (ReLU)
+        col = torch.rand(n, s, 3, generator=g)
+        _, zz = renderer.sample_points_on_rays(torch.zeros(n, 3), torch.ones(n, 3), s)
+        dd = torch.randn(n, 3, generator=g)
+        cases[f"rand{s}"] = (sig, col, zz.contiguous(), dd)
+    s = 64
+    n = 8
+    _, zz = renderer.sample_points_on_rays(torch.zeros(n, 3), torch.ones(n, 3), s)
+    dd = torch.randn(n, 3, generator=g)
+    col = torch.rand(n, s, 3, generator=g)
+    edge = torch.zeros(n, s, 1)
+    edge[1] = 1e4                                  # huge density everywhere
+    edge[2, -1] = 5.0                              # density only at the last sample (dist 1e10)
+    edge[3, -1] = 1e-9                             # tiny density at the last sample
+    edge[4, :, 0] = torch.linspace(-1, 1, s)       # ramp through zero
+    edge[5, 10] = 50.0                             # a single opaque slab
+    edge[6] = 1e-7
+    edge[7, :, 0] = torch.tensor([1e-30 * (k + 1) for k in range(s)])   # denormal-ish
+    cases["edge64"] = (edge, col, zz.contiguous(), dd)
+    for name, (sig, col, zz, dd) in cases.items():
+        rgb, depth = renderer.execute_volume_rendering(sig, col, zz, dd)
+        rgb2, depth2, acc, wts = vr.volume_render(sig, col, zz, dd)
+        comp[f"{name}_sigma"] = sig.numpy()
+        comp[f"{name}_rgb_in"] = col.numpy()
+        comp[f"{name}_z"] = zz.numpy()
+        comp[f"{name}_d"] = dd.numpy()
+        comp[f"{name}_rgb"] = rgb.numpy()
+        comp[f"{name}_depth"] = depth.numpy()
+        comp[f"{name}_acc"] = acc.numpy()
+        comp[f"{name}_weights"] = wts.numpy()
+        assert torch.equal(rgb, rgb2) and torch.equal(depth, depth2)
+    save("composite.npz", **comp)
+
+    # ---- stratified (perturbed) sampling with captured t_rand -----------------
+    ro_s, rd_s = renderer.generate_rays(poses[0], 16, 8)
+    ro_s, rd_s = ro_s.reshape(-1, 3), rd_s.reshape(-1, 3)
+    torch.manual_seed(7)
+    pts_s, z_s = vr.sample_points_on_rays(ro_s, rd_s, 2.0, 6.0, 32, perturb=True)
+    torch.manual_seed(7)
+    t_rand = torch.rand(ro_s.shape[0], 32)
+    save("stratified.npz", rays_o=ro_s.numpy(), rays_d=rd_s.numpy(), t_rand=t_rand.numpy(),
+         z=z_s.numpy(), pts=pts_s.numpy())
+
+    # ---- full renders --------------------------------------------------------
+    timing = {}
+    for (w, h, s, pose_ids) in [(64, 48, 16, [0, 1, 2]), (37, 23, 7, [2]), (200, 150, 32, [0, 1, 2]),
+                                (400, 300, 64, [0])]:
+        out = {"poses": pose_arr[pose_ids], "pose_ids": np.array(pose_ids, dtype=np.int32),
+               "W": np.int32(w), "H": np.int32(h), "S": np.int32(s)}
+        for k, pi in enumerate(pose_ids):
+            t0 = time.time()
+            rgb, depth = renderer.render_image(poses[pi], (w, h), s)
+            timing[f"{w}x{h}x{s}_view{pi}"] = time.time() - t0
+            out[f"rgb_{k}"] = rgb.numpy()
+            out[f"depth_{k}"] = depth.numpy()
+        save(f"render_{w}x{h}_s{s}.npz", **out)
+
+    # a band of the 800x600x128 headline image, rendered with the reference's own
+    # per-chunk path on rows [296, 304) only (chunking is result-neutral: SURVEY a7)
+    band = {"rows": np.array([296, 304], dtype=np.int32), "W": np.int32(800), "H": np.int32(600),
+            "S": np.int32(128), "poses": pose_arr[[0, 2]]}
+    for k, pi in enumerate([0, 2]):
+        ro, rd = renderer.generate_rays(poses[pi], 800, 600)
+        ro = ro[296:304].reshape(-1, 3)
+        rd = rd[296:304].reshape(-1, 3)
+        rgbs, depths = [], []
+        for c in range(0, ro.shape[0], 512):
+            r_, d_ = renderer._render_ray_chunk(ro[c:c + 512], rd[c:c + 512], 128)
+            rgbs.append(r_)
+            depths.append(d_)
+        band[f"rgb_{k}"] = torch.cat(rgbs).reshape(8, 800, 3).numpy()
+        band[f"depth_{k}"] = torch.cat(depths).reshape(8, 800).numpy()
+    save("render_800x600_s128_band.npz", **band)
+
+    meta["render_seconds"] = timing
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")

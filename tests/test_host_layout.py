@@ -1,0 +1,240 @@
+"""Host-side checks of the C ABI library -- no GPU needed.
+
+* the library loads and exports every symbol include/nerf_mi355x.h declares;
+* the z table helper reproduces the reference's z values bit for bit;
+* the weight packer (the same C++ code nerf_ctx_load_weights runs) produces
+  fragment blobs that, pushed through a numpy emulation of the kernels'
+  MFMA lane maps, compute exactly the NeRF MLP.  This pins the packing and the
+  k-order permutations on CPU; the GPU tests then pin the kernels themselves.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from nerf_amd import runtime as rt
+from nerf_amd import weights as W
+from oracle import nerf_oracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "nerf_mi355x.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nerf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_binding():
+    assert declared_functions() == sorted(rt.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = rt.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.nerf_abi_version() == 1
+
+
+def test_uniform_z_bit_exact(golden):
+    g = golden("tvals")
+    for s in [1, 2, 3, 16, 32, 64, 128, 192, 256]:
+        assert np.array_equal(rt.uniform_z(g[f"t_{s}"], 2.0, 6.0), g[f"z_{s}"]), s
+
+
+def test_pack_rejects_bad_input():
+    sd = W.synthetic_state_dict(3)
+    bad = dict(sd)
+    bad["layers.4.weight"] = np.zeros((256, 318), np.float32)
+    with pytest.raises(ValueError):
+        rt.pack_weights(bad)
+
+
+# ---------------------------------------------------------------- layout spec --
+# Python statement of nerf_layout.h (the kernels' register maps).
+def acc_row(r, h):
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+def pe_slot_feature(h, q):
+    if q < 30:
+        return 3 + 6 * (5 * h + q // 6) + (q % 6)
+    if h == 0:
+        return q - 30
+    return 2 if q == 30 else -1
+
+
+def dpe_slot_feature(h, q):
+    if q < 12:
+        return 3 + 6 * (2 * h + q // 6) + (q % 6)
+    if h == 0:
+        return q - 12 if q < 14 else -1
+    return 2 if q == 12 else -1
+
+
+LAYERS = [  # (spec prefix, out, hidden, extra)
+    ("layers.0", 256, 0, "pos"), ("layers.1", 256, 256, None), ("layers.2", 256, 256, None),
+    ("layers.3", 256, 256, None), ("layers.4", 256, 256, "pos"), ("layers.5", 256, 256, None),
+    ("layers.6", 256, 256, None), ("layers.7", 256, 256, None), ("color_layers.0", 128, 256, "dir"),
+]
+
+
+def bf16_to_f32(u16):
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+def round_bf16(x):
+    return bf16_to_f32((torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.bfloat16)
+                        .view(torch.int16).numpy().view(np.uint16)))
+
+
+def slot_values(feats, h, n_slots, slot_fn):
+    """[n_slots, ncols] values lane half h supplies (0 for padding)."""
+    out = np.zeros((n_slots, feats.shape[1]))
+    for q in range(n_slots):
+        f = slot_fn(h, q)
+        if f >= 0:
+            out[q] = feats[f]
+    return out
+
+
+def unpack_bias(prm, layer, nt):
+    b = np.zeros(32 * nt)
+    for o in range(nt):
+        for h in range(2):
+            for r in range(16):
+                b[32 * o + acc_row(r, h)] = prm[256 * layer + (o * 2 + h) * 16 + r]
+    return b
+
+
+def heads(prm, x, hcol):
+    """density and colour heads from the packed param blob (fp32 VALU path)."""
+    sig_w, c1_w = np.zeros(256), np.zeros((3, 128))
+    for h in range(2):
+        for t in range(8):
+            for r in range(16):
+                sig_w[32 * t + acc_row(r, h)] = prm[2304 + (h * 8 + t) * 16 + r]
+        for c in range(3):
+            for t in range(4):
+                for r in range(16):
+                    c1_w[c, 32 * t + acc_row(r, h)] = prm[2564 + ((c * 2 + h) * 4 + t) * 16 + r]
+    sigma = np.maximum(sig_w @ x + prm[2560], 0)
+    rgb = 1 / (1 + np.exp(-(c1_w @ hcol + prm[2948:2951, None])))
+    return sigma, rgb
+
+
+def emulate(f32_blob, bf16_blob, prm, pe, dpe, precision):
+    """Run the packed network the way the kernels' lane maps do.  pe [63, n], dpe [27, n]."""
+    n = pe.shape[1]
+    x = None
+    off_f32, off_bf16 = 0, 0
+    for li, (_, out, hidden, extra) in enumerate(LAYERS):
+        nt = out // 32
+        n_ext = {"pos": 32, "dir": 16, None: 0}[extra]
+        ext = [None, None]
+        if extra:
+            feats, fn = (pe, pe_slot_feature) if extra == "pos" else (dpe, dpe_slot_feature)
+            ext = [slot_values(feats, h, n_ext, fn) for h in range(2)]
+        acc = np.tile(unpack_bias(prm, li, nt)[:, None], (1, n))
+        if precision == "fp32":
+            ku = hidden // 2 + n_ext
+            a = f32_blob[off_f32: off_f32 + ku * nt * 64].reshape(ku // 4, nt, 2, 32, 4)
+            off_f32 += ku * nt * 64
+            a = a.transpose(0, 4, 1, 2, 3).reshape(ku, nt, 2, 32)          # [u, o, k(h), i]
+            for u in range(ku):
+                for h in range(2):
+                    if u < hidden // 2:
+                        b = x[32 * (u >> 4) + acc_row(u & 15, h)]
+                    else:
+                        b = ext[h][u - hidden // 2]
+                    acc += np.einsum("oi,j->oij", a[u, :, h], b).reshape(32 * nt, n)
+        else:
+            ku = hidden // 16 + n_ext // 8
+            chunks = -(-ku * nt * 1024 // 16384)
+            raw = bf16_blob[off_bf16: off_bf16 + ku * nt * 512]
+            off_bf16 += chunks * 8192
+            a = bf16_to_f32(raw).reshape(ku, nt, 2, 32, 8)                  # [u, o, h, i, j]
+            xr = None if x is None else round_bf16(x)
+            for u in range(ku):
+                for h in range(2):
+                    for j in range(8):
+                        if u < hidden // 16:
+                            b = xr[32 * (u >> 1) + 16 * (u & 1) + 8 * (j >> 2) + 4 * h + (j & 3)]
+                        else:
+                            b = round_bf16(ext[h][8 * (u - hidden // 16) + j])
+                        acc += np.einsum("oi,j->oij", a[u, :, h, :, j], b).reshape(32 * nt, n)
+        acc = np.maximum(acc, 0)
+        if li == 7:
+            x7 = acc
+        x = acc
+    sigma, rgb = heads(prm, x7, x)
+    return sigma, rgb
+
+
+def direct(sd, pe, dpe, rnd):
+    """Plain restatement with the precision's rounding applied at MFMA inputs."""
+    x = pe
+    for i in range(8):
+        if i == 4:
+            x = np.concatenate([x, pe])
+        x = np.maximum(rnd(sd[f"layers.{i}.weight"]).astype(np.float64) @ rnd(x) + sd[f"layers.{i}.bias"][:, None], 0)
+    sigma = np.maximum(sd["density_head.weight"].astype(np.float64) @ x + sd["density_head.bias"][:, None], 0)[0]
+    hcol = np.maximum(rnd(sd["color_layers.0.weight"]).astype(np.float64) @ rnd(np.concatenate([x, dpe]))
+                      + sd["color_layers.0.bias"][:, None], 0)
+    rgb = 1 / (1 + np.exp(-(sd["color_layers.1.weight"].astype(np.float64) @ hcol + sd["color_layers.1.bias"][:, None])))
+    return sigma, rgb
+
+
+@pytest.fixture(scope="module")
+def packed():
+    sd = W.synthetic_state_dict(1)
+    return sd, rt.pack_weights(sd)
+
+
+@pytest.fixture(scope="module")
+def samples(golden):
+    g = golden("mlp")
+    idx = np.linspace(0, g["pos"].shape[0] - 1, 24).astype(int)
+    pos, dirs = torch.from_numpy(g["pos"][idx]), torch.from_numpy(g["dirs"][idx])
+    return (O.positional_encoding(pos, 10).numpy().T.astype(np.float64),
+            O.positional_encoding(dirs, 4).numpy().T.astype(np.float64), g, idx)
+
+
+def test_packed_sizes():
+    sd = W.synthetic_state_dict(1)
+    f32, bf, prm = rt.pack_weights(sd)
+    assert f32.size * 4 == 8 * 0 + sum(((h // 2 + {"pos": 32, "dir": 16, None: 0}[e]) * (o // 32) * 64 * 4)
+                                       for _, o, h, e in LAYERS)
+    assert bf.size * 2 == 65 * 16384
+    assert prm.size == 2952
+
+
+def test_fp32_packing_computes_the_mlp(packed, samples):
+    sd, (f32, bf, prm) = packed
+    pe, dpe, _, _ = samples
+    s_emu, rgb_emu = emulate(f32, bf, prm, pe, dpe, "fp32")
+    s_dir, rgb_dir = direct(sd, pe, dpe, lambda a: np.asarray(a, np.float64))
+    np.testing.assert_allclose(s_emu, s_dir, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(rgb_emu, rgb_dir, rtol=1e-9, atol=1e-9)
+
+
+def test_bf16_packing_computes_the_mlp(packed, samples):
+    sd, (f32, bf, prm) = packed
+    pe, dpe, _, _ = samples
+    s_emu, rgb_emu = emulate(f32, bf, prm, pe, dpe, "bf16")
+    s_dir, rgb_dir = direct(sd, pe, dpe, lambda a: round_bf16(a).astype(np.float64))
+    np.testing.assert_allclose(s_emu, s_dir, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(rgb_emu, rgb_dir, rtol=1e-6, atol=1e-6)
+
+
+def test_fp32_emulation_matches_reference_golden(samples):
+    """The packed fine net through the emulated lane maps reproduces the reference's outputs."""
+    pe, dpe, g, idx = samples
+    c, f = W.synthetic_models(0)
+    f32, bf, prm = rt.pack_weights(f)
+    s_emu, rgb_emu = emulate(f32, bf, prm, pe, dpe, "fp32")
+    np.testing.assert_allclose(s_emu, g["sigma_fine"][idx, 0], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(rgb_emu.T, g["rgb_fine"][idx], rtol=0, atol=1e-6)

@@ -1,0 +1,132 @@
+"""Pin the oracle (oracle/nerf_oracle.py) to golden vectors produced by the reference.
+
+The fixtures come from tests/golden/make_golden.py, which ran the reference's
+own renderer, model and volume-render code on the synthetic checkpoint.  The
+oracle must reproduce them bit-for-bit where the arithmetic is deterministic
+element-wise work (rays, t/z tables, stratified samples, the whole pipeline on
+this host) and to fp32 rounding otherwise (a different host's GEMM kernels may
+sum in another order).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+from nerf_amd import weights as W
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 2e-6     # fp32 rounding slack for GEMM/transcendental kernels of another host
+
+
+@pytest.fixture(scope="module")
+def nets():
+    c, f = W.synthetic_models(0)
+    return O.Net(c), O.Net(f)
+
+
+def test_checkpoint_digest_matches_fixtures():
+    meta = json.load(open(os.path.join(GOLDEN, "golden_meta.json")))
+    c, f = W.synthetic_models(0)
+    assert W.state_dict_digest(c) == meta["coarse_digest"]
+    assert W.state_dict_digest(f) == meta["fine_digest"]
+
+
+def test_rays_bit_exact(golden):
+    g = golden("rays")
+    keys = [k for k in g.files if k.startswith("o_")]
+    assert len(keys) == 9
+    for k in keys:
+        tag = k[2:]
+        w, h = map(int, tag.split("_")[0].split("x"))
+        pi = int(tag.split("_")[1])
+        o, d = O.generate_rays(g["poses"][pi], w, h)
+        assert np.array_equal(o.numpy(), g[k]), tag
+        assert np.array_equal(d.numpy(), g["d_" + tag]), tag
+
+
+@pytest.mark.parametrize("s", [1, 2, 3, 16, 32, 64, 128, 192, 256])
+def test_tvals_and_z_bit_exact(golden, s):
+    g = golden("tvals")
+    assert np.array_equal(O.t_vals(s).numpy(), g[f"t_{s}"])
+    assert np.array_equal(O.uniform_z(s).numpy(), g[f"z_{s}"])
+
+
+def test_stratified_samples_bit_exact(golden):
+    g = golden("stratified")
+    z = O.stratified_z(O.uniform_z(32), torch.from_numpy(g["t_rand"]))
+    assert np.array_equal(z.numpy(), g["z"])
+    pts = O.sample_points(torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"]), z)
+    assert np.array_equal(pts.numpy(), g["pts"])
+
+
+def test_positional_encoding(golden):
+    g = golden("pe")
+    x = torch.from_numpy(g["x"])
+    for L, key in ((10, "pe10"), (4, "pe4")):
+        pe = O.positional_encoding(x, L).numpy()
+        assert pe.shape == g[key].shape == (x.shape[0], 3 + 6 * L)
+        np.testing.assert_allclose(pe, g[key], rtol=0, atol=TOL)
+
+
+def test_mlp_forward(golden, nets):
+    g = golden("mlp")
+    coarse, fine = nets
+    for net, tag in ((fine, "fine"), (coarse, "coarse")):
+        s, rgb = O.nerf_forward(net, torch.from_numpy(g["pos"]), torch.from_numpy(g["dirs"]))
+        np.testing.assert_allclose(s.numpy(), g[f"sigma_{tag}"], rtol=1e-6, atol=1e-5)
+        np.testing.assert_allclose(rgb.numpy(), g[f"rgb_{tag}"], rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("case", ["rand16", "rand32", "rand64", "rand128", "edge64"])
+def test_composite(golden, case):
+    g = golden("composite")
+    rgb, depth, acc, w = O.composite(g[f"{case}_sigma"], g[f"{case}_rgb_in"], g[f"{case}_z"], g[f"{case}_d"], True)
+    np.testing.assert_allclose(rgb.numpy(), g[f"{case}_rgb"], rtol=0, atol=TOL)
+    np.testing.assert_allclose(depth.numpy(), g[f"{case}_depth"], rtol=0, atol=4 * TOL)
+    np.testing.assert_allclose(acc.numpy(), g[f"{case}_acc"], rtol=0, atol=TOL)
+    np.testing.assert_allclose(w.numpy(), g[f"{case}_weights"], rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("name", ["render_64x48_s16", "render_37x23_s7", "render_200x150_s32"])
+def test_full_render(golden, nets, name):
+    g = golden(name)
+    _, fine = nets
+    w, h, s = int(g["W"]), int(g["H"]), int(g["S"])
+    for k in range(len(g["pose_ids"])):
+        rgb, depth = O.render_image(fine, g["poses"][k], (w, h), s)
+        np.testing.assert_allclose(rgb.numpy(), g[f"rgb_{k}"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(depth.numpy(), g[f"depth_{k}"], rtol=0, atol=1e-5)
+
+
+def test_headline_band(golden, nets):
+    """Rows 296..303 of the 800x600x128 headline image (reference's chunked path)."""
+    g = golden("render_800x600_s128_band")
+    _, fine = nets
+    r0, r1 = map(int, g["rows"])
+    for k in range(2):
+        rgb, depth = O.render_image(fine, g["poses"][k], (800, 600), 128, rows=(r0, r1))
+        np.testing.assert_allclose(rgb.numpy(), g[f"rgb_{k}"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(depth.numpy(), g[f"depth_{k}"], rtol=0, atol=1e-5)
+
+
+def test_importance_sample_properties():
+    """Build-defined hierarchical sampler (reference crashes): parity unpinned
+    beyond these properties -- sorted union, coarse z preserved, samples inside [near, far]."""
+    torch.manual_seed(0)
+    n, s, ni = 64, 64, 128
+    z = O.uniform_z(s).expand(n, s).contiguous()
+    w = torch.rand(n, s) ** 4
+    u = O.default_u(n, ni)
+    zi = O.importance_sample(z, w, u)
+    assert zi.shape == (n, ni)
+    assert torch.all(zi[:, 1:] >= zi[:, :-1])           # monotone in ascending u
+    assert torch.all((zi >= 2.0) & (zi <= 6.0))
+    zf = O.fine_z(z, w, u)
+    assert zf.shape == (n, s + ni)
+    assert torch.all(zf[:, 1:] >= zf[:, :-1])
+    # every coarse sample survives the merge
+    for r in range(0, n, 16):
+        assert set(z[r].tolist()) <= set(zf[r].tolist())
