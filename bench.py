@@ -130,6 +130,15 @@ def main():
 
     flop_launch = band_rays * spp * W.FLOPS_PER_SAMPLE
     kern_ms = float(np.mean(mlp_ms))
+    traffic, traffic_src = None, None
+    kname = f"mlp_{args.precision}_kernel"
+    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc) and (width, height, spp, world) == (800, 600, 128, 1):
+        k = json.load(open(pmc))["kernels"].get(kname, {})
+        if "hbm_bytes_per_launch" in k:
+            traffic = k["hbm_bytes_per_launch"]
+            traffic_src = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench "
+                           f"({json.load(open(pmc))['source']}); bytes/launch, FETCH x2 (gfx950)")
     achieved = flop_launch / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
 
@@ -171,8 +180,8 @@ def main():
                        "resolution": [width, height], "samples_per_ray": spp,
                        "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
-                         "kernel": f"mlp_{args.precision}_kernel", "kernel_ms": kern_ms,
+                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": kname, "kernel_ms": kern_ms,
                          "flop_per_launch": flop_launch},
             "cpu_baseline": cpu,
         }

@@ -218,8 +218,8 @@ int nerf_composite(const float* sigma, int sigma_stride, const float* rgb, int r
 
 int nerf_importance_sample(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
                            int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine, void* stream) {
-  if (n_rays < 0 || n_coarse <= 0 || n_coarse > 256 || n_importance < 0)
-    return set_error(NERF_E_INVALID, "nerf_importance_sample: bad sizes (n_coarse must be 1..256)");
+  if (n_rays < 0 || n_coarse < 2 || n_coarse > 256 || n_importance < 0)
+    return set_error(NERF_E_INVALID, "nerf_importance_sample: bad sizes (n_coarse must be 2..256)");
   if (n_rays == 0) return NERF_OK;
   if (!z_coarse || !weights || !z_fine || (n_importance > 0 && !u))
     return set_error(NERF_E_INVALID, "nerf_importance_sample: null pointer");
@@ -256,7 +256,7 @@ int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
   if (width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 > row1)
     return set_error(NERF_E_INVALID, "nerf_render: bad image/rows %dx%d [%d,%d)", width, height, row0, row1);
   if (n_samples <= 0 || n_samples > 1024 || n_importance < 0 || n_importance > 1024 ||
-      (n_importance > 0 && n_samples > 256))
+      (n_importance > 0 && (n_samples < 2 || n_samples > 256)))
     return set_error(NERF_E_INVALID, "nerf_render: bad sample counts %d+%d", n_samples, n_importance);
   const long n_rays = long(row1 - row0) * width;
   if (n_rays == 0) return NERF_OK;

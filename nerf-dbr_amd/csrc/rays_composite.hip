@@ -34,8 +34,10 @@ __global__ void rays_kernel(Pose pose, int width, float half_w, float half_h, fl
   }
 }
 
-// execute_volume_rendering (pytorch_renderers.py:105-125): one thread per ray,
-// transmittance as the sequential exclusive product (torch.cumprod order).
+// execute_volume_rendering (pytorch_renderers.py:105-125): one thread per ray.
+// Transmittance is the exclusive product of (1 - alpha + 1e-10) accumulated the
+// way torch's CPU cumprod does it: sequentially in double, each output rounded
+// to fp32 (ATen cpu_cum_base_kernel uses acc_type<float> = double).
 __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stride, const float* __restrict__ rgb,
                                  int rgb_stride, const float* __restrict__ z, int z_ray_stride,
                                  const float* __restrict__ rays_d, int n_rays, int n_samples,
@@ -43,18 +45,29 @@ __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stri
                                  float* __restrict__ acc_out, float* __restrict__ weights_out) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
+  if (n_samples == 1) {
+    // The reference's quirk, kept for drop-in parity: with one sample,
+    // `dists[..., :1]` of the empty difference tensor is empty, so every
+    // per-sample array is empty and the image is all zeros
+    // (pytorch_renderers.py:107-108; same in rendering.py:105-106).
+    rgb_out[3L * r] = rgb_out[3L * r + 1] = rgb_out[3L * r + 2] = 0.0f;
+    depth_out[r] = 0.0f;
+    if (acc_out) acc_out[r] = 0.0f;
+    return;
+  }
   const float dx = rays_d[3L * r], dy = rays_d[3L * r + 1], dz = rays_d[3L * r + 2];
   const float norm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
   const float* zr = z + long(r) * z_ray_stride;
   const long base = long(r) * n_samples;
-  float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, dep = 0.0f, acc = 0.0f;
+  double T_acc = 1.0;
+  float cr = 0.0f, cg = 0.0f, cb = 0.0f, dep = 0.0f, acc = 0.0f;
   float z_cur = zr[0];
   for (int s = 0; s < n_samples; ++s) {
     const float z_next = s + 1 < n_samples ? zr[s + 1] : 0.0f;
     const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(z_next, z_cur) : 1e10f, norm);
     const float sg = relu(sigma[(base + s) * sigma_stride]);
     const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-sg, dist)));
-    const float w = __fmul_rn(alpha, T);
+    const float w = __fmul_rn(alpha, float(T_acc));
     const float* c = rgb + (base + s) * rgb_stride;
     cr = __fadd_rn(cr, __fmul_rn(w, c[0]));
     cg = __fadd_rn(cg, __fmul_rn(w, c[1]));
@@ -62,7 +75,7 @@ __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stri
     dep = __fadd_rn(dep, __fmul_rn(w, z_cur));
     acc = __fadd_rn(acc, w);
     if (weights_out) weights_out[base + s] = w;
-    T = __fmul_rn(T, __fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f));
+    T_acc = __dmul_rn(T_acc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
     z_cur = z_next;
   }
   rgb_out[3L * r] = cr;
@@ -73,7 +86,8 @@ __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stri
 }
 
 // Fixed VolumeRenderer.importance_sample (rendering.py:54-100; the reference's
-// gather at :89-90 crashes): pdf = (w+1e-5)/sum, sequential sum and cumsum;
+// gather at :89-90 crashes): pdf = (w+1e-5)/sum; the sum and the cdf are
+// torch-CPU cumsums (sequential, double accumulator, fp32 outputs);
 // u ascending per ray (inverse CDF is monotone, so the importance samples come
 // out sorted and merge with the sorted coarse z in one pass).
 constexpr int kMaxCoarse = 256;
@@ -88,10 +102,15 @@ __global__ void importance_kernel(const float* __restrict__ z_coarse, int z_ray_
   const float* ur = u + long(r) * u_ray_stride;
   float* out = z_fine + long(r) * (n_coarse + n_importance);
   float cdf[kMaxCoarse + 1];
-  float total = 0.0f;
-  for (int i = 0; i < n_coarse; ++i) total = __fadd_rn(total, __fadd_rn(wr[i], 1e-5f));
+  double sum = 0.0;
+  for (int i = 0; i < n_coarse; ++i) sum = __dadd_rn(sum, double(__fadd_rn(wr[i], 1e-5f)));
+  const float total = float(sum);
   cdf[0] = 0.0f;
-  for (int i = 0; i < n_coarse; ++i) cdf[i + 1] = __fadd_rn(cdf[i], __fdiv_rn(__fadd_rn(wr[i], 1e-5f), total));
+  sum = 0.0;
+  for (int i = 0; i < n_coarse; ++i) {
+    sum = __dadd_rn(sum, double(__fdiv_rn(__fadd_rn(wr[i], 1e-5f), total)));
+    cdf[i + 1] = float(sum);
+  }
   int ic = 0;        // next coarse sample to emit
   int o = 0;
   int lo = 0;        // searchsorted hint: u ascending

@@ -168,6 +168,28 @@ class MI355XRenderer(BaseUnifiedRenderer):
             self.hip.composite(sig, 1, col, 3, z, s, d, n, s, rgb, depth, acc, w)
         return (rgb, depth, acc, w) if with_weights else (rgb, depth)
 
+    def render_rays_z(self, rays_o, rays_d, z, use_fine: bool = True, with_weights: bool = False):
+        """MLP + compositing for explicit rays [N,3] and per-ray samples z [N,S] (the
+        body of _render_ray_chunk, pytorch_renderers.py:156-170, with z given)."""
+        import torch
+
+        dev = torch.device("cuda", self.device_index)
+        o = rays_o.to(dev, torch.float32).reshape(-1, 3).contiguous()
+        d = rays_d.to(dev, torch.float32).reshape(-1, 3).contiguous()
+        zz = z.to(dev, torch.float32).contiguous()
+        n, s = zz.shape
+        out = torch.empty(n * s, 4, dtype=torch.float32, device=dev)
+        net = rt.NERF_NET_FINE if use_fine else rt.NERF_NET_COARSE
+        with torch.cuda.device(self.device_index):
+            self.hip.mlp_forward(net, rt.PRECISIONS[self.precision], o, d, zz, s, n, s, out)
+        rgb = torch.empty(n, 3, dtype=torch.float32, device=dev)
+        depth = torch.empty(n, dtype=torch.float32, device=dev)
+        acc = torch.empty(n, dtype=torch.float32, device=dev) if with_weights else None
+        w = torch.empty(n, s, dtype=torch.float32, device=dev) if with_weights else None
+        with torch.cuda.device(self.device_index):
+            self.hip.composite(out, 4, out[:, 1:], 4, zz, s, d, n, s, rgb, depth, acc, w)
+        return (rgb, depth, acc, w) if with_weights else (rgb, depth)
+
     def importance_sample(self, z_coarse, weights, u):
         """Fixed VolumeRenderer.importance_sample (rendering.py:54-100): sorted union [N, S+Ni].
         ``u`` [N, Ni] or [Ni], ascending along the last axis."""

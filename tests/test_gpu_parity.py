@@ -139,22 +139,56 @@ def test_importance_sampler_matches_oracle(r32):
         assert np.array_equal(got.cpu().numpy(), ref.numpy())
 
 
-def test_render_hierarchical_vs_oracle(ckpt):
-    """64+128 on a small image, fp32: pipeline parity with the oracle's hierarchical render.
-    The fine samples depend on the coarse net's weights, so fp32 summation-order
-    differences can move them; the tolerance is looser than the uniform path's."""
+def test_hierarchical_stage_by_stage(r32):
+    """64+128-style pipeline checked stage by stage against the oracle, each stage fed
+    the oracle's inputs: coarse weights, importance samples (bit-exact), fine image."""
+    from oracle import nerf_oracle as O
+
+    c, f = W.synthetic_models(0)
+    coarse, fine = O.Net(c), O.Net(f)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
+    o, d = O.generate_rays(pose, 48, 20)
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    n, nc, ni = o.shape[0], 64, 128
+    zc = O.uniform_z(nc).expand(n, nc).contiguous()
+    # coarse pass -> weights
+    pts = O.sample_points(o, d, zc)
+    s_, c_ = O.nerf_forward(coarse, pts.reshape(-1, 3), d[:, None].expand_as(pts).reshape(-1, 3))
+    _, _, _, w_ref = O.composite(s_.reshape(n, nc, 1), c_.reshape(n, nc, 3), zc, d, True)
+    _, _, _, w_gpu = r32.render_rays_z(o, d, zc, use_fine=False, with_weights=True)
+    ew = maxabs(w_gpu, w_ref.numpy())
+    # importance samples from the oracle's weights: bit-exact
+    u = O.default_u(n, ni)
+    zf_ref = O.fine_z(zc, w_ref, u)
+    zf_gpu = r32.importance_sample(zc, w_ref, u.contiguous())
+    assert np.array_equal(zf_gpu.cpu().numpy(), zf_ref.numpy())
+    # fine pass on the oracle's fine samples
+    pts = O.sample_points(o, d, zf_ref)
+    s_, c_ = O.nerf_forward(fine, pts.reshape(-1, 3), d[:, None].expand_as(pts).reshape(-1, 3))
+    rgb_ref, dep_ref = O.composite(s_.reshape(n, -1, 1), c_.reshape(n, -1, 3), zf_ref, d)
+    rgb_gpu, dep_gpu = r32.render_rays_z(o, d, zf_ref)
+    er, ed = maxabs(rgb_gpu, rgb_ref.numpy()), maxabs(dep_gpu, dep_ref.numpy())
+    print(f"hierarchical stages: coarse weights {ew:.2e}, fine rgb {er:.2e} depth {ed:.2e}")
+    assert ew < 1e-4 and er < TOL_RENDER and ed < TOL_RENDER
+
+
+def test_render_hierarchical_end_to_end(ckpt):
+    """Whole 64+128 render vs the oracle.  The fine samples are placed by the coarse
+    net's weights, so fp32 summation-order differences in the coarse MLP move them
+    (by ~1e-6 in z, amplified by the 2^9*pi position encoding); parity is therefore
+    asserted stage by stage above and only loosely here."""
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
     from oracle import nerf_oracle as O
 
-    r = MI355XRenderer("fp32", n_importance=32)
+    r = MI355XRenderer("fp32", n_importance=128)
     r.setup(ckpt)
     c, f = W.synthetic_models(0)
-    pose = O._t(np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 4.0], [0, 0, 0, 1]], np.float32))
-    rgb, depth = r.render_image(pose, (40, 30), 16)
-    ref_rgb, ref_depth = O.render_image_hierarchical(O.Net(c), O.Net(f), pose, (40, 30), 16, 32)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][0])
+    rgb, depth = r.render_image(pose, (40, 30), 64)
+    ref_rgb, ref_depth = O.render_image_hierarchical(O.Net(c), O.Net(f), pose, (40, 30), 64, 128)
     er, ed = maxabs(rgb, ref_rgb.numpy()), maxabs(depth, ref_depth.numpy())
-    print(f"hierarchical 40x30 16+32: rgb {er:.3e} depth {ed:.3e}")
-    assert er < 1e-3 and ed < 1e-3
+    print(f"hierarchical end-to-end 40x30 64+128: rgb {er:.3e} depth {ed:.3e}")
+    assert er < 2e-2 and ed < 2e-2
 
 
 def test_headline_full_size_properties(r16):

@@ -1,0 +1,160 @@
+"""CPU tests of the host-side logic: checkpoints, the plugin interface, the suite's
+CSV/rays-per-second contract and the multi-process band gather (gloo, world size 2)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from nerf_amd import distributed as D
+from nerf_amd import weights as W
+from nerf_amd.benchmark import base_renderer as B
+from nerf_amd.benchmark.benchmark_suite import CSV_COLUMNS, UnifiedBenchmarkSuite, generate_test_poses
+
+
+def test_param_counts():
+    assert W.N_PARAMS == 530052
+    assert W.FLOPS_PER_SAMPLE == 1055744
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    c, f = W.synthetic_models(5)
+    p = W.save_checkpoint(str(tmp_path / "ck.pth"), c, f)
+    c2, f2 = W.load_checkpoint(p)
+    assert W.state_dict_digest(c) == W.state_dict_digest(c2)
+    assert W.state_dict_digest(f) == W.state_dict_digest(f2)
+
+
+def test_checkpoint_reference_layout_with_extra_keys(tmp_path):
+    """Trainer checkpoints carry optimizer/config entries too (trainer.py:376-384)."""
+    c, f = W.synthetic_models(1)
+    ck = {"coarse_model": {k: torch.from_numpy(v) for k, v in c.items()},
+          "fine_model": {k: torch.from_numpy(v) for k, v in f.items()},
+          "config": {"lr": 5e-4, "n_samples": 64}, "train_losses": [0.1, 0.05], "val_losses": []}
+    p = str(tmp_path / "trainer.pth")
+    torch.save(ck, p)
+    c2, f2 = W.load_checkpoint(p)
+    assert W.state_dict_digest(f) == W.state_dict_digest(f2)
+
+
+def test_strict_state_dict():
+    sd = W.synthetic_state_dict(0)
+    del sd["density_head.bias"]
+    with pytest.raises(KeyError):
+        W.validate_state_dict(sd)
+
+
+def test_shared_model_missing_checkpoint_falls_back(tmp_path, capsys):
+    B.SharedNeRFModel.reset()
+    m = B.SharedNeRFModel()
+    m.load_models(str(tmp_path / "nope.pth"), "cuda")
+    coarse, fine = m.get_models("cuda")
+    assert "randomly initialized" in capsys.readouterr().out
+    W.validate_state_dict(coarse)
+    B.SharedNeRFModel.reset()
+
+
+def test_mi355x_renderer_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    with pytest.raises(RuntimeError):
+        MI355XRenderer("bf16")
+
+
+def test_poses_match_reference_fixture(golden):
+    g = golden("rays")
+    poses = generate_test_poses(2)
+    for i in range(2):
+        assert np.array_equal(poses[i].numpy(), g["poses"][i])
+
+
+class FakeRenderer(B.BaseUnifiedRenderer):
+    """CPU stand-in that only exercises the suite's plumbing."""
+
+    def __init__(self):
+        super().__init__("Fake", "cpu")
+
+    def render_image(self, camera_pose, resolution, samples_per_ray=64):
+        w, h = resolution
+        return torch.full((h, w, 3), 0.5), torch.full((h, w), 3.0)
+
+    def execute_volume_rendering(self, densities, colors, z_vals, ray_directions):
+        raise NotImplementedError
+
+    def query_nerf_networks(self, positions, directions, use_fine=True):
+        raise NotImplementedError
+
+    def generate_rays(self, camera_pose, width, height, focal=800.0):
+        raise NotImplementedError
+
+    def sample_points_on_rays(self, rays_o, rays_d, n_samples=64):
+        raise NotImplementedError
+
+
+def test_suite_csv_contract(tmp_path):
+    ck = W.write_synthetic_checkpoint(str(tmp_path / "ck.pth"))
+    suite = UnifiedBenchmarkSuite(str(tmp_path / "out"), warmup=0)
+    suite.renderers.append(FakeRenderer())
+    suite.run_benchmark(ck, [(20, 10)], [8], n_views=2)
+    df = suite.generate_report(plot=False)
+    assert list(df.columns) == CSV_COLUMNS
+    row = df.iloc[0]
+    assert row["Resolution"] == "20x10" and row["Samples/Ray"] == 8
+    assert np.isclose(row["Rays/Second"], 200 / row["Render Time (s)"])
+    assert os.path.exists(tmp_path / "out" / "benchmark_results.csv")
+    assert os.path.exists(tmp_path / "out" / "sample_renders" / "Fake" / "view_1_rgb.png")
+
+
+@pytest.mark.parametrize("world,height", [(1, 600), (2, 600), (8, 600), (8, 150), (3, 7), (4, 2)])
+def test_bands_partition_rows(world, height):
+    b = D.bands(world, height)
+    assert b[0][0] == 0 and b[-1][1] == height
+    assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+    assert max(r1 - r0 for r0, r1 in b) - min(r1 - r0 for r0, r1 in b) <= 1
+
+
+def _gather_worker(rank, world, port, width, height, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def render_rows(pose, res, spp, r0, r1):
+        rows = torch.arange(r0, r1, dtype=torch.float32)[:, None].expand(r1 - r0, width)
+        cols = torch.arange(width, dtype=torch.float32)[None, :].expand(r1 - r0, width)
+        rgb = torch.stack([rows, cols, rows * 1000 + cols], -1)
+        return rgb, rows + 0.5
+
+    rgb, depth = D.render_sharded(render_rows, None, (width, height), 4)
+    q.put((rank, rgb.numpy(), depth.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("height", [10, 7])
+def test_band_gather_gloo_world2(height):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    width = 5
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, width, height, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rows = np.arange(height, dtype=np.float32)[:, None].repeat(width, 1)
+    cols = np.arange(width, dtype=np.float32)[None, :].repeat(height, 0)
+    for _, rgb, depth in outs:
+        assert np.array_equal(rgb, np.stack([rows, cols, rows * 1000 + cols], -1))
+        assert np.array_equal(depth, rows + 0.5)
