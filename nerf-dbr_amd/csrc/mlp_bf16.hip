@@ -9,53 +9,102 @@
 //
 // Geometry: 256-thread workgroups (4 waves, one per SIMD) of 256 samples; a
 // wave owns two 32-sample column tiles, so every A (weight) fragment it reads
-// feeds two MFMAs.  A lane keeps one layer's 2x8 accumulator tiles (256 fp32)
-// and the previous layer as packed bf16 B fragments (128 VGPRs): activations
-// never leave registers (nerf_layout.h).  The position encoding waits in LDS
-// for layers 0 and 4.
+// feeds two MFMAs.  A lane keeps one layer's 2x8 accumulator tiles (256 fp32,
+// AGPRs) and the previous layer as packed bf16 B fragments (128 VGPRs):
+// activations never leave registers (nerf_layout.h).  The position and
+// direction encodings wait in LDS for the layers that take them.
 //
-// Weight stream: the packed 1.04 MB blob is cut into 16 KiB chunks (2 k-steps
-// of a 256-wide layer).  A 4-slot LDS ring is filled by global_load_lds_dwordx4
-// (lane-linear 1 KiB pieces) three chunks ahead; one raw s_barrier per chunk
-// publishes the chunk two ahead (counted vmcnt, never 0 in the loop), and the
-// first k-step's fragments of the next chunk are read before that barrier, so
-// ds_read latency never stalls the MFMA pipe at a chunk seam.  Per chunk a SIMD
-// runs 32 MFMAs (1024 cycles) against 16 KiB of L2->LDS traffic per CU.
+// Quarter schedule.  Each layer is issued in quarters of two output tiles.
+// The previous layer's accumulators are converted to bf16 fragments (ReLU'd),
+// and that conversion is VALU work the MFMA pipe would otherwise wait on.  Only
+// tiles 0-1 are converted up front; tiles 2-7 are converted in 12 slices
+// interleaved with quarter 0's MFMAs (their registers are first overwritten in
+// quarter 1, and k-step 2t first reads tile t's fragments after its slice).
+//
+// Weight stream.  The packed blob is a sequence of 2 KiB units (layer, quarter,
+// k-step) cut into 16 KiB chunks.  A 4-slot LDS ring is filled by
+// global_load_lds_dwordx4 (lane-linear 1 KiB pieces) three chunks ahead; one raw
+// s_barrier per chunk publishes the chunk two ahead (counted vmcnt, never 0 in
+// the loop).  Fragments are prefetched two units ahead through a 3-entry
+// register ring, across chunk seams.
 #include "nerf_device.h"
 #include "nerf_internal.h"
 
 namespace nerf {
 namespace {
 
-constexpr int kWaves = 4;
+#ifndef NERF_BF16_WAVES
+#define NERF_BF16_WAVES 8            // 8: two waves per SIMD, 32 samples each; 4: one per SIMD, 64 each
+#endif
+constexpr int kWaves = NERF_BF16_WAVES;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kCols = 2;                                   // column tiles per wave
-constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;   // 256
-constexpr int kTotalChunks = bf16_blob_chunks();
-constexpr int kSlots = 4, kAhead = 3;                      // ring slots, load lookahead (chunks)
-constexpr int kGldsPerStage = kChunkBytes / (kThreads * 16);   // 4 per wave
-constexpr int kLdsParamOff = kSlots * kChunkBytes;
+constexpr int kCols = 8 / kWaves;                                     // column tiles per wave
+static_assert(kCols == 1 || kCols == 2, "4 or 8 waves");
+constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
+// Ring geometry (compile-time knobs, swept with tools/kernel_lab.py).
+#ifndef NERF_BF16_CHUNK_UNITS
+#define NERF_BF16_CHUNK_UNITS 8      // 2 KiB units per LDS chunk (one barrier per chunk)
+#endif
+#ifndef NERF_BF16_SLOTS
+#define NERF_BF16_SLOTS 4            // chunk slots in the LDS ring
+#endif
+#ifndef NERF_BF16_AHEAD
+#define NERF_BF16_AHEAD 3            // chunks in flight ahead of the one being read
+#endif
+#ifndef NERF_BF16_PF
+#define NERF_BF16_PF 2               // fragment prefetch distance (units)
+#endif
+constexpr int kUnits = bf16_unit_base(kNumMfmaLayers);                // 516
+constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
+constexpr int kChunkB = kChunkUnits * kUnitBytes;
+constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
+constexpr int kSlots = NERF_BF16_SLOTS, kAhead = NERF_BF16_AHEAD;
+constexpr int kPf = NERF_BF16_PF;
+constexpr int kRing = kPf + 1;
+constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // LDS-DMA pieces per wave per chunk
+constexpr int kLdsParamOff = kSlots * kChunkB;
+static_assert(kSlots >= kAhead + 1, "a slot is restaged only after every read of its previous chunk");
+static_assert(kAhead >= 2 && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
+static_assert(kTotalChunks * kChunkB <= kBf16BlobBytes, "device blob is padded for every chunk geometry");
 constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kCols * 4 * 1024;
-constexpr int kLdsBytes = kLdsDeOff + kWaves * kCols * 2 * 1024;
+constexpr int kLdsStampOff = kLdsDeOff + kWaves * kCols * 2 * 1024;
+#ifdef NERF_STAMPS
+constexpr int kLdsBytes = kLdsStampOff + kWaves * (2 + 3 * kTotalChunks + 1) * 8;
+#else
+constexpr int kLdsBytes = kLdsStampOff;
+#endif
 static_assert(kLdsParamOff % 16 == 0 && kLdsPeOff % 16 == 0, "LDS carve must stay 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
-static_assert(kGldsPerStage * kThreads * 16 == kChunkBytes, "stage geometry");
-
-template <int L>
-constexpr int bf16_chunk0() {
-  int c = 0;
-  for (int l = 0; l < L; ++l) c += bf16_layer_chunks(l);
-  return c;
-}
+static_assert(kGldsPerStage * kThreads * 16 == kChunkB, "stage geometry");
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// Chunk g -> ring slot g % kSlots.  Each wave moves 4 KiB as four lane-linear
+// ---- compile-time unit map (constant-folded after unrolling) ----
+NL_HD int unit_layer(int n) {
+  int l = 0;
+  while (l + 1 < kNumMfmaLayers && bf16_unit_base(l + 1) <= n) ++l;
+  return l;
+}
+NL_HD int unit_kstep(int n) { return (n - bf16_unit_base(unit_layer(n))) % ksteps_bf16(unit_layer(n)); }
+NL_HD int unit_extra(int n) {   // 0: B from hidden fragments; else the Extra kind
+  const int l = unit_layer(n);
+  return unit_kstep(n) < layer_shape(l).hidden / 16 ? 0 : layer_shape(l).extra;
+}
+
+// Chunk g -> ring slot g % kSlots.  Each wave moves its share as lane-linear
 // 1 KiB LDS-DMA pieces (destination = wave-uniform base + lane*16).
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
-  const char* src = blob + size_t(g) * kChunkBytes + wave_u * 1024 + lane * 16;
-  char* dst = lds + (g % kSlots) * kChunkBytes + wave_u * 1024;
+#ifdef NERF_ABLATE_HOTCHUNK   // timing experiment: every chunk re-reads chunk 0 (L2-hot, wrong results)
+  const char* src = blob + wave_u * 1024 + lane * 16;
+#else
+  const char* src = blob + size_t(g) * kChunkB + wave_u * 1024 + lane * 16;
+#endif
+  char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i)
     __builtin_amdgcn_global_load_lds((const void*)(src + i * kThreads * 16), (lds_void*)(dst + i * kThreads * 16),
@@ -71,29 +120,48 @@ __device__ __forceinline__ bf16x8 pack8(const float* v) {
   return r;
 }
 
-// ReLU'd accumulators -> next layer's B fragments (register 8s..8s+7 of tile t
-// is k-step 2t+s; nerf_layout.h hid_bf16_feature).
-__device__ __forceinline__ void to_fragments(const f32x16 (&acc)[kCols][8], bf16x8 (&bh)[kCols][16]) {
-#pragma unroll
-  for (int c = 0; c < kCols; ++c)
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = relu(acc[c][t][8 * s + j]);
-        bh[c][2 * t + s] = pack8(v);
-      }
+// ReLU after rounding, on the packed bf16 words: RNE rounding preserves sign
+// and order, so relu(bf16(x)) == bf16(relu(x)) bit for bit, and a bf16 is
+// negative exactly when its bit pattern is a negative int16 -> v_pk_max_i16
+// with 0 (one instruction per two values, no fp32 canonicalisation).
+__device__ __forceinline__ unsigned cvt_relu_pair(float lo, float hi) {
+  const bf16x2 p = __builtin_convertvector(f32x2{lo, hi}, bf16x2);                    // v_cvt_pk_bf16_f32
+  const i16x2 m = __builtin_elementwise_max(__builtin_bit_cast(i16x2, p), i16x2(0));   // v_pk_max_i16
+  return __builtin_bit_cast(unsigned, m);
 }
 
-// The k-step fragments of one chunk-slot: NT tiles x 1 KiB, this lane's 16 B each.
-// (nt is a constant after unrolling)
-__device__ __forceinline__ void read_frags(bf16x8 (&a)[8], const char* slot_lane, int uu, int nt) {
-#pragma unroll
-  for (int o = 0; o < 8; ++o)
-    if (o < nt) a[o] = *(const bf16x8*)(slot_lane + (uu * nt + o) * 1024);
+__device__ __forceinline__ bf16x8 pack8_relu(const f32x16& a, int base) {
+#if defined(NERF_ABLATE_EPILOGUE) || defined(NERF_ABLATE_LOOPONLY)
+  // timing experiment: raw bits of 4 accumulator registers (every tile stays
+  // live, so no MFMA is dead-code eliminated), no conversion, no ReLU
+  return __builtin_bit_cast(bf16x8, f32x4{a[base], a[base + 1], a[base + 2], a[base + 3]});
+#else
+  const u32x4 w{cvt_relu_pair(a[base], a[base + 1]), cvt_relu_pair(a[base + 2], a[base + 3]),
+                cvt_relu_pair(a[base + 4], a[base + 5]), cvt_relu_pair(a[base + 6], a[base + 7])};
+  return __builtin_bit_cast(bf16x8, w);
+#endif
 }
+
+// ---- diagnostic build only (-DNERF_STAMPS): s_memtime at the prologue end and
+// on both sides of every chunk barrier, per wave, for the first 256 blocks.
+// Never compiled into the shipped library; its times are not quoted, its
+// shares are (cdna_hip_programming.md §7, In-kernel stamps).
+[[maybe_unused]] constexpr int kStampSlots = 2 + 3 * kTotalChunks + 1;
+#ifdef NERF_STAMPS
+constexpr int kStampBlocks = 256;
+constexpr unsigned kStampFirst = 8192;   // steady state: well past the cold-L2 first wave of blocks
+__device__ unsigned long long g_nerf_stamps[kStampBlocks][kWaves][kStampSlots];
+#define NERF_STAMP(cx, i)                                                                             \
+  do {                                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                                \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                       \
+    if ((cx).lane == 0)                                                                               \
+      ((unsigned long long*)((cx).lds + kLdsStampOff))[(cx).wave_u * kStampSlots + (i)] = t_;         \
+    __builtin_amdgcn_sched_barrier(0);                                                                \
+  } while (0)
+#else
+#define NERF_STAMP(cx, i) do {} while (0)
+#endif
 
 struct Ctx {
   const char* blob;
@@ -101,68 +169,147 @@ struct Ctx {
   int wave_u, lane, h;
 };
 
-// End of chunk g: publish chunk g+2, prefetch the first k-step of chunk g+1.
-__device__ __forceinline__ void chunk_seam(const Ctx& cx, int g, bf16x8 (&a)[8], int nt_next) {
-  // stage(g+2) must have landed; stage(g+3) (issued at the start of g) may fly.
-  if (g + kAhead < kTotalChunks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGldsPerStage) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this wave's reads of slot g are done
-  if (g + 1 < kTotalChunks) read_frags(a, cx.lds + ((g + 1) % kSlots) * kChunkBytes + cx.lane * 16, 0, nt_next);
-  compiler_fence();
-  __builtin_amdgcn_s_barrier();
-  compiler_fence();
+// Tile t of column c of the previous layer -> B fragments 2t, 2t+1 (register
+// 8s..8s+7 of tile t is k-step 2t+s; nerf_layout.h hid_bf16_feature).  Before
+// colour layer 0 the tile also feeds the density head (fp32, nerf.py:114).
+template <bool kDensity>
+__device__ __forceinline__ void convert_tile(const f32x16& acc_t, bf16x8& b0, bf16x8& b1, float& dens,
+                                             const Ctx& cx, int t) {
+  b0 = pack8_relu(acc_t, 0);
+  b1 = pack8_relu(acc_t, 8);
+  if (kDensity) {
+    const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = w4[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dens = fmaf(w[i], relu(acc_t[4 * q + i]), dens);
+    }
+    // pin the partial sum here: sinking these FMAs to the kernel's end would keep
+    // the layer's accumulators alive through C0 (and spill them)
+    asm volatile("" : "+v"(dens));
+  }
 }
 
-// Extra (non-hidden) inputs live in LDS: 4 position-encoding k-steps per
-// column tile at kLdsPeOff, 2 direction-encoding k-steps at kLdsDeOff.
-template <int L, int NT, int NT_NEXT>
-__device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], const bf16x8 (&bh)[kCols][16],
-                                           bf16x8 (&a)[8], const Ctx& cx) {
+// Reads of unit n into ring entry n % kRing: two A fragments (output tiles of
+// the unit's quarter) and, for encoding inputs, the two columns' B fragments.
+__device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols]) {
+  const char* slot = cx.lds + ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes + cx.lane * 16;
+  ra[n % kRing][0] = *(const bf16x8*)(slot);
+  ra[n % kRing][1] = *(const bf16x8*)(slot + 1024);
+  const int ex = unit_extra(n);
+  if (ex != 0) {
+    const int u = unit_kstep(n) - layer_shape(unit_layer(n)).hidden / 16;
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      const int off = ex == kPos ? kLdsPeOff + ((cx.wave_u * kCols + c) * 4 + u) * 1024
+                                 : kLdsDeOff + ((cx.wave_u * kCols + c) * 2 + u) * 1024;
+      rb[n % kRing][c] = *(const bf16x8*)(cx.lds + off + cx.lane * 16);
+    }
+  }
+}
+
+// s_waitcnt vmcnt(k) for a k that is a constant only after unrolling.
+__device__ __forceinline__ void wait_vmcnt(int k) {
+#define NERF_VM(N) else if (k == N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");
+  if (k <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  NERF_VM(1) NERF_VM(2) NERF_VM(3) NERF_VM(4) NERF_VM(5) NERF_VM(6) NERF_VM(7) NERF_VM(8)
+  NERF_VM(10) NERF_VM(12) NERF_VM(14) NERF_VM(15) NERF_VM(16) NERF_VM(18) NERF_VM(20) NERF_VM(21)
+  NERF_VM(24) NERF_VM(28) NERF_VM(30) NERF_VM(32)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef NERF_VM
+}
+
+// Chunks whose LDS-DMA may still be in flight after stage(g+2) has landed:
+// stage(g+3 .. g+kAhead), as far as they were issued.
+NL_HD int stages_after(int g) {
+  const int last = (g + kAhead < kTotalChunks - 1) ? g + kAhead : kTotalChunks - 1;
+  return last > g + 2 ? last - (g + 2) : 0;
+}
+
+// After unit n: when it closes chunk g, (1) this wave's reads of slot g are
+// complete (lgkmcnt(0): the slot is restaged after the barrier), (2) its own
+// pieces of chunk g+2 have landed (counted vmcnt), (3) the barrier publishes
+// chunk g+2 to every wave, then (4) chunk g+1+kAhead starts loading into the
+// slot chunk g+1+kAhead-kSlots used.
+__device__ __forceinline__ void after_unit(const Ctx& cx, int n) {
+  if ((n + 1) % kChunkUnits != 0 || n + 1 >= kUnits) return;
+  const int g = n / kChunkUnits;
+  NERF_STAMP(cx, 2 + 3 * g);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wait_vmcnt(kGldsPerStage * stages_after(g));
+  compiler_fence();
+  NERF_STAMP(cx, 3 + 3 * g);
+#if !defined(NERF_ABLATE_BARRIER) && !defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no chunk barrier
+  __builtin_amdgcn_s_barrier();
+#endif
+  compiler_fence();
+  NERF_STAMP(cx, 4 + 3 * g);
+  if (g + 1 + kAhead < kTotalChunks) stage_chunk(cx.blob, g + 1 + kAhead, cx.lds, cx.wave_u, cx.lane);
+}
+
+template <int L>
+__device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)[kCols][16],
+                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], float (&dens)[kCols],
+                                           const Ctx& cx) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
   constexpr int KU = ksteps_bf16(L);
-  constexpr int UPC = kChunkBytes / (NT * 1024);     // k-steps per chunk
-  constexpr int NCH = bf16_layer_chunks(L);
-  constexpr int G0 = bf16_chunk0<L>();
+  constexpr int NQ = out_tiles(L) / 2;
+  constexpr int N0 = bf16_unit_base(L);
+  constexpr bool kConvert = L != L0;          // B fragments come from the previous layer
+  constexpr bool kDensity = L == C0;          // ... which, before C0, also feeds the density head
   const float* prm = (const float*)(cx.lds + kLdsParamOff);
+  if (kConvert) {
+    // This wave's reads of the previous layer's last units are issued; the
+    // conversion of tiles 0-1 is the only part not hidden behind MFMAs.
 #pragma unroll
-  for (int c = 0; c < kCols; ++c) load_bias<NT>(acc[c], prm, L, cx.h);
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-  for (int ch = 0; ch < NCH; ++ch) {
-    const int g = G0 + ch;
-    if (g + kAhead < kTotalChunks) stage_chunk(cx.blob, g + kAhead, cx.lds, cx.wave_u, cx.lane);
-    const char* slot_lane = cx.lds + (g % kSlots) * kChunkBytes + cx.lane * 16;
+      for (int c = 0; c < kCols; ++c) convert_tile<kDensity>(acc[c][t], bh[c][2 * t], bh[c][2 * t + 1], dens[c], cx, t);
+  }
 #pragma unroll
-    for (int uu = 0; uu < UPC; ++uu) {
-      const int u = ch * UPC + uu;
-      if (u < KU) {
-        bf16x8 an[8];
-        if (uu + 1 < UPC && u + 1 < KU) read_frags(an, slot_lane, uu + 1, NT);
-        bf16x8 b[kCols];
+  for (int q = 0; q < NQ; ++q) {
+    // bias pre-load of this quarter's two output tiles (both columns)
 #pragma unroll
-        for (int c = 0; c < kCols; ++c) {
-          if (u < KH) {
-            b[c] = bh[c][u < KH ? u : 0];
-          } else if (sh.extra == kPos) {
-            b[c] = *(const bf16x8*)(cx.lds + kLdsPeOff + ((cx.wave_u * kCols + c) * 4 + (u - KH)) * 1024 +
-                                    cx.lane * 16);
-          } else {
-            b[c] = *(const bf16x8*)(cx.lds + kLdsDeOff + ((cx.wave_u * kCols + c) * 2 + (u - KH)) * 1024 +
-                                    cx.lane * 16);
-          }
-        }
+    for (int o2 = 0; o2 < 2; ++o2) {
+      const f32x4* b4 = (const f32x4*)(prm + kBiasOff + 256 * L + ((2 * q + o2) * 2 + cx.h) * 16);
 #pragma unroll
-        for (int o = 0; o < NT; ++o)
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 b = b4[i];
 #pragma unroll
-          for (int c = 0; c < kCols; ++c)
-            acc[c][o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[o], b[c], acc[c][o], 0, 0, 0);
-        if (uu + 1 < UPC && u + 1 < KU) {
+        for (int c = 0; c < kCols; ++c)
 #pragma unroll
-          for (int o = 0; o < NT; ++o) a[o] = an[o];
-        }
+          for (int e = 0; e < 4; ++e) acc[c][2 * q + o2][4 * i + e] = b[e];
       }
     }
-    chunk_seam(cx, g, a, ch + 1 < NCH ? NT : NT_NEXT);
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int n = N0 + q * KU + u;
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+#ifndef NERF_BF16_NO_SCHED_PIN
+      // keep the prefetch reads here: left alone, the scheduler sinks them next
+      // to their MFMAs and every unit then waits out the LDS latency
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      bf16x8 b[kCols];
+#pragma unroll
+      for (int c = 0; c < kCols; ++c) b[c] = u < KH ? bh[c][u < KH ? u : 0] : rb[n % kRing][c];
+#pragma unroll
+      for (int o2 = 0; o2 < 2; ++o2)
+#pragma unroll
+        for (int c = 0; c < kCols; ++c)
+          acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][o2], b[c], acc[c][2 * q + o2],
+                                                                      0, 0, 0);
+      // conversion slices: the (tile, column) pairs of tiles 2..7 spread over
+      // k-steps 0..11, one tile per two k-steps (tile t done before k-step 2t)
+      if (kConvert && q == 0 && u < 12 && (u % (2 / kCols)) == 0) {
+        const int i = u / (2 / kCols);
+        const int t = 2 + i / kCols, c = i % kCols;
+        convert_tile<kDensity>(acc[c][t], bh[c][2 * t], bh[c][2 * t + 1], dens[c], cx, t);
+      }
+      after_unit(cx, n);
+    }
   }
 }
 
@@ -176,6 +323,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   const int h = lane >> 5;
   const Ctx cx{blob, lds, wave_u, lane, h};
   const long p0 = (long(blockIdx.x) * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
+  NERF_STAMP(cx, 0);
 
   // Kick off the weight stream, then do the per-sample prologue under it.
 #pragma unroll
@@ -188,8 +336,15 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     const long p = p0 + c * kSamplesPerWave;
     float x[3], d[3], pef[32], def[16];
     fetch_sample<kExplicit>(src, p < n_points ? p : n_points - 1, x, d);
-    pos_encode(x[0], x[1], x[2], h, pef);
-    dir_encode(d[0], d[1], d[2], h, def);
+#if defined(NERF_ABLATE_ENCODING) || defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no sin/cos
+#pragma unroll
+    for (int q = 0; q < 32; ++q) pef[q] = x[q % 3] * float(q);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) def[q] = d[q % 3] * float(q);
+#else
+    pos_encode<true>(x[0], x[1], x[2], h, pef);
+    dir_encode<true>(d[0], d[1], d[2], h, def);
+#endif
     char* pe_dst = lds + kLdsPeOff + (wave_u * kCols + c) * 4096 + lane * 16;
     char* de_dst = lds + kLdsDeOff + (wave_u * kCols + c) * 2048 + lane * 16;
 #pragma unroll
@@ -197,46 +352,45 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     *(bf16x8*)(de_dst) = pack8(def);
     *(bf16x8*)(de_dst + 1024) = pack8(def + 8);
   }
-  // chunks 0 and 1 published; first fragments of chunk 0 in registers
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGldsPerStage) : "memory");
+  // chunks 0 and 1 published (later stages may still fly); prime the fragment ring
+  wait_vmcnt(kGldsPerStage * (kAhead - 2));
   __syncthreads();
-  bf16x8 a[8];
-  read_frags(a, lds + lane * 16, 0, 8);
+  NERF_STAMP(cx, 1);
+  bf16x8 ra[kRing][2], rb[kRing][kCols];
+#pragma unroll
+  for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+  stage_chunk(blob, kAhead, lds, wave_u, lane);   // the start of chunk 0
 
   f32x16 acc[kCols][8];
   bf16x8 bh[kCols][16];
-  layer_bf16<L0, 8, 8>(acc, bh, a, cx);
-  to_fragments(acc, bh);
-  layer_bf16<L1, 8, 8>(acc, bh, a, cx);
-  to_fragments(acc, bh);
-  layer_bf16<L2, 8, 8>(acc, bh, a, cx);
-  to_fragments(acc, bh);
-  layer_bf16<L3, 8, 8>(acc, bh, a, cx);
-  to_fragments(acc, bh);
-  layer_bf16<L4, 8, 8>(acc, bh, a, cx);   // skip: [x, pe] (nerf.py:109-110)
-  to_fragments(acc, bh);
-  layer_bf16<L5, 8, 8>(acc, bh, a, cx);
-  to_fragments(acc, bh);
-  layer_bf16<L6, 8, 8>(acc, bh, a, cx);
-  to_fragments(acc, bh);
-  layer_bf16<L7, 8, 4>(acc, bh, a, cx);
+  float dens[kCols];
+#pragma unroll
+  for (int c = 0; c < kCols; ++c) dens[c] = 0.0f;
+  layer_bf16<L0>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<L1>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<L2>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<L3>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<L4>(acc, bh, ra, rb, dens, cx);   // skip: [x, pe] (nerf.py:109-110)
+  layer_bf16<L5>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<L6>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<L7>(acc, bh, ra, rb, dens, cx);
+  layer_bf16<C0>(acc, bh, ra, rb, dens, cx);   // [x, PE4(d)] (nerf.py:117-121); density head folded in
   const float* prm = (const float*)(lds + kLdsParamOff);
-  float sigma[kCols];
 #pragma unroll
   for (int c = 0; c < kCols; ++c) {
-    relu_tiles<8>(acc[c]);
-    sigma[c] = density_head(acc[c], prm, h);
-  }
-  to_fragments(acc, bh);
-  layer_bf16<C0, 4, 4>(acc, bh, a, cx);   // [x, PE4(d)] (nerf.py:117-121)
-#pragma unroll
-  for (int c = 0; c < kCols; ++c) {
+    const float sigma = relu(dens[c] + __shfl_xor(dens[c], 32) + prm[kSigB]);
     relu_tiles<4>(acc[c]);
     float rgb[3];
     color_head(acc[c], prm, h, rgb);
     const long p = p0 + c * kSamplesPerWave;
-    if (p < n_points && h == 0) out[p] = f32x4{sigma[c], rgb[0], rgb[1], rgb[2]};
+    if (p < n_points && h == 0) out[p] = f32x4{sigma, rgb[0], rgb[1], rgb[2]};
   }
+#ifdef NERF_STAMPS
+  NERF_STAMP(cx, kStampSlots - 1);
+  if (blockIdx.x - kStampFirst < kStampBlocks && lane == 0)
+    for (int i = 0; i < kStampSlots; ++i)
+      g_nerf_stamps[blockIdx.x - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
+#endif
 }
 
 }  // namespace
@@ -257,3 +411,14 @@ hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSr
 }
 
 }  // namespace nerf
+
+#ifdef NERF_STAMPS
+// diagnostic build only: copy the stamps out ([256 blocks][waves][slots] u64)
+extern "C" int nerf_debug_stamps(void* host, size_t bytes, int* waves, int* slots) {
+  *waves = nerf::kWaves;
+  *slots = nerf::kStampSlots;
+  const size_t need = sizeof(nerf::g_nerf_stamps);
+  if (bytes < need) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nerf::g_nerf_stamps), need) == hipSuccess ? 0 : -2;
+}
+#endif

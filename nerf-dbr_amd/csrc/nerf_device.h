@@ -21,9 +21,32 @@ __device__ __forceinline__ float sample_coord(float o, float d, float z) {
   return __fadd_rn(o, __fmul_rn(d, z));
 }
 
+// sin and cos of an fp32 argument, for the bf16 path (whose encodings are
+// rounded to bf16, 2^-9 relative): exact Cody-Waite reduction by 2*pi
+// (6.28125 + 0.00193500518798828125 + 3.0199160e-07; q < 2^12 for |a| < 2^14.6,
+// the products are exact), then the hardware v_sin/v_cos on revolutions in
+// [-1/2, 1/2].  Error ~1e-6 absolute vs the correctly rounded value.
+__device__ __forceinline__ void sincos_fast(float a, float* s, float* c) {
+  const float q = __builtin_rintf(__fmul_rn(a, 0.15915493667125702f));
+  float r = fmaf(-q, 6.28125f, a);
+  r = fmaf(-q, 0.0019350051879882812f, r);
+  r = fmaf(-q, 3.019916050561733e-07f, r);
+  const float t = __fmul_rn(r, 0.15915493667125702f);
+  *s = __builtin_amdgcn_sinf(t);
+  *c = __builtin_amdgcn_cosf(t);
+}
+
+// sin/cos of fl(2^k*pi)*x: accurate ocml sincosf (the fp32 parity path) or the
+// reduced-precision sincos_fast (the bf16 path).
+template <bool kFast>
+__device__ __forceinline__ void pe_sincos(float c, float x, float* s, float* co) {
+  if (kFast) sincos_fast(__fmul_rn(c, x), s, co);
+  else sincosf(__fmul_rn(c, x), s, co);
+}
+
 // Position encoding slots of lane half h (nerf_layout.h pe_slot_feature):
-// 15 sin/cos pairs + the raw coordinates it owns.  Accurate sincosf (ocml),
-// never the hardware v_sin/v_cos approximations.
+// 15 sin/cos pairs + the raw coordinates it owns.
+template <bool kFast = false>
 __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, float (&pe)[32]) {
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
@@ -32,7 +55,7 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       float s, co;
-      sincosf(__fmul_rn(c, xs[m]), &s, &co);
+      pe_sincos<kFast>(c, xs[m], &s, &co);
       pe[6 * kk + m] = s;
       pe[6 * kk + 3 + m] = co;
     }
@@ -41,6 +64,7 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
   pe[31] = h ? 0.0f : x1;
 }
 
+template <bool kFast = false>
 __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, float (&de)[16]) {
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
@@ -49,7 +73,7 @@ __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, 
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       float s, co;
-      sincosf(__fmul_rn(c, ds[m]), &s, &co);
+      pe_sincos<kFast>(c, ds[m], &s, &co);
       de[6 * kk + m] = s;
       de[6 * kk + 3 + m] = co;
     }

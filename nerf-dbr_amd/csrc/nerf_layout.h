@@ -103,9 +103,13 @@ NL_HD int bf16_k_col(int l, int u, int h, int j) {
 // ---------------------------------------------------------------- packing --
 // f32 A blob, per layer: [u/4][tile o][lane 64][4 floats]  (one float4 per lane
 //   covers four consecutive k-steps).
-// bf16 A blob, per layer: [u][tile o][lane 64][8 bf16]; the whole stream is cut
-//   into 16 KiB chunks consumed in order (2 k-steps of a 256-out layer, 4 of C0);
-//   C0 is zero-padded to whole chunks.
+// bf16 A blob: a stream of 2 KiB "units", one per (layer, quarter q, k-step u):
+//   per layer [q][u][tile-in-quarter o2 (2)][lane 64][8 bf16], where quarter q
+//   holds output tiles 2q and 2q+1 (4 quarters for 256-wide layers, 2 for C0).
+//   Issuing a layer quarter by quarter lets the previous layer's accumulator
+//   tiles 2..7 be converted while quarter 0 computes (mlp_bf16.hip).  The
+//   stream is cut into 16 KiB chunks (8 units) consumed in order; the tail is
+//   zero-padded to a whole chunk.
 // Params blob (fp32, shared by both precisions), in floats:
 //   bias[layer l][tile o][half h][16]  at  kBiasOff + 256*l (C0: 128 used)
 //   density weight [h][tile t][16] at kSigW, density bias at kSigB
@@ -118,10 +122,15 @@ constexpr int kC1W = kSigB + 4;                     // 16-B aligned
 constexpr int kC1B = kC1W + 3 * 128;
 constexpr int kParamFloats = kC1B + 4;              // 2952
 
+constexpr int kUnitBytes = 2048;                    // one k-step of one quarter
+constexpr int kUnitsPerChunk = kChunkBytes / kUnitBytes;
+
 NL_HD int f32_layer_floats(int l) { return ksteps_f32(l) * out_tiles(l) * 64; }
-NL_HD int bf16_layer_chunks(int l) {
-  int bytes = ksteps_bf16(l) * out_tiles(l) * 1024;
-  return (bytes + kChunkBytes - 1) / kChunkBytes;
+NL_HD int bf16_layer_units(int l) { return (out_tiles(l) / 2) * ksteps_bf16(l); }
+NL_HD int bf16_unit_base(int l) {                   // first unit of layer l
+  int n = 0;
+  for (int i = 0; i < l; ++i) n += bf16_layer_units(i);
+  return n;
 }
 NL_HD int f32_blob_floats() {
   int n = 0;
@@ -129,9 +138,10 @@ NL_HD int f32_blob_floats() {
   return n;
 }
 NL_HD int bf16_blob_chunks() {
-  int n = 0;
-  for (int l = 0; l < kNumMfmaLayers; ++l) n += bf16_layer_chunks(l);
-  return n;
+  return (bf16_unit_base(kNumMfmaLayers) + kUnitsPerChunk - 1) / kUnitsPerChunk;
 }
+// Packed bf16 blob size: units rounded up to a multiple of 32 (zero padding),
+// so any kernel chunk geometry of up to 32 units reads inside the buffer.
+constexpr int kBf16BlobBytes = ((bf16_unit_base(kNumMfmaLayers) + 31) / 32) * 32 * kUnitBytes;
 
 }  // namespace nerf

@@ -31,7 +31,7 @@ uint16_t f32_to_bf16_rne(float f) {
 
 extern "C" void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob) {
   if (f32_blob) *f32_blob = size_t(f32_blob_floats()) * sizeof(float);
-  if (bf16_blob) *bf16_blob = size_t(bf16_blob_chunks()) * kChunkBytes;
+  if (bf16_blob) *bf16_blob = size_t(kBf16BlobBytes);
   if (param_blob) *param_blob = size_t(kParamFloats) * sizeof(float);
 }
 
@@ -57,21 +57,21 @@ extern "C" int nerf_pack_weights(const float* const* params, int n_params, float
     }
   }
   if (bf16_blob) {
-    uint16_t* base = bf16_blob;
+    uint16_t* dst = bf16_blob;
     for (int l = 0; l < kNumMfmaLayers; ++l) {
-      const int spec = kSpecOfLayer[l], nt = out_tiles(l), ku = ksteps_bf16(l);
-      uint16_t* dst = base;
-      for (int u = 0; u < ku; ++u)
-        for (int o = 0; o < nt; ++o)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int j = 0; j < 8; ++j) {
-              const int col = bf16_k_col(l, u, lane >> 5, j);
-              *dst++ = col < 0 ? uint16_t(0) : f32_to_bf16_rne(W(spec, 32 * o + (lane & 31), col));
-            }
-      uint16_t* end = base + size_t(bf16_layer_chunks(l)) * (kChunkBytes / 2);
-      while (dst < end) *dst++ = 0;
-      base = end;
+      const int spec = kSpecOfLayer[l], nq = out_tiles(l) / 2, ku = ksteps_bf16(l);
+      for (int q = 0; q < nq; ++q)
+        for (int u = 0; u < ku; ++u)
+          for (int o2 = 0; o2 < 2; ++o2)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int j = 0; j < 8; ++j) {
+                const int col = bf16_k_col(l, u, lane >> 5, j);
+                const int row = 32 * (2 * q + o2) + (lane & 31);
+                *dst++ = col < 0 ? uint16_t(0) : f32_to_bf16_rne(W(spec, row, col));
+              }
     }
+    uint16_t* end = bf16_blob + size_t(kBf16BlobBytes) / 2;
+    while (dst < end) *dst++ = 0;
   }
   if (param_blob) {
     std::memset(param_blob, 0, sizeof(float) * kParamFloats);

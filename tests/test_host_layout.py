@@ -153,10 +153,11 @@ def emulate(f32_blob, bf16_blob, prm, pe, dpe, precision):
                     acc += np.einsum("oi,j->oij", a[u, :, h], b).reshape(32 * nt, n)
         else:
             ku = hidden // 16 + n_ext // 8
-            chunks = -(-ku * nt * 1024 // 16384)
             raw = bf16_blob[off_bf16: off_bf16 + ku * nt * 512]
-            off_bf16 += chunks * 8192
-            a = bf16_to_f32(raw).reshape(ku, nt, 2, 32, 8)                  # [u, o, h, i, j]
+            off_bf16 += ku * nt * 512
+            # stream order [quarter q][u][tile-in-quarter][lane][8] -> [u, o, h, i, j]
+            a = bf16_to_f32(raw).reshape(nt // 2, ku, 2, 2, 32, 8).transpose(1, 0, 2, 3, 4, 5)
+            a = a.reshape(ku, nt, 2, 32, 8)
             xr = None if x is None else round_bf16(x)
             for u in range(ku):
                 for h in range(2):
@@ -208,7 +209,7 @@ def test_packed_sizes():
     f32, bf, prm = rt.pack_weights(sd)
     assert f32.size * 4 == 8 * 0 + sum(((h // 2 + {"pos": 32, "dir": 16, None: 0}[e]) * (o // 32) * 64 * 4)
                                        for _, o, h, e in LAYERS)
-    assert bf.size * 2 == 65 * 16384
+    assert bf.size * 2 == 544 * 2048          # 516 units padded to a multiple of 32
     assert prm.size == 2952
 
 
