@@ -106,9 +106,30 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
 #endif
   char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
 #pragma unroll
-  for (int i = 0; i < kGldsPerStage; ++i)
+  for (int i = 0; i < kGldsPerStage; ++i) {
+#ifdef NERF_BF16_BUILTIN_GLDS
     __builtin_amdgcn_global_load_lds((const void*)(src + i * kThreads * 16), (lds_void*)(dst + i * kThreads * 16),
                                      16, 0, 0);
+#else
+    // Issued from inline asm: when hipcc sees an LDS-DMA in a function it stops
+    // counting LDS waits and emits lgkmcnt(0) before every fragment use.  The DMA
+    // completion is tracked by hand (counted vmcnt + barrier at each seam); an asm
+    // VMEM op can only make hipcc's own vmcnt waits stricter, never looser.
+    // M0 (the LDS base) is set and restored inside the statement (§5.7).
+    unsigned keep;
+    const unsigned lds_addr = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(dst + i * kThreads * 16));
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src + i * kThreads * 16), "s"(lds_addr)
+        : "memory");
+#endif
+  }
 }
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
@@ -227,6 +248,35 @@ NL_HD int stages_after(int g) {
   return last > g + 2 ? last - (g + 2) : 0;
 }
 
+#ifndef NERF_BF16_SEAM_OLD
+// Seam E_g, at the top of unit n when its prefetch (unit n+kPf) is the first
+// unit of chunk g+1.  Every read of chunk g-1 was consumed by MFMAs of earlier
+// units (so no lgkmcnt wait), so after the barrier its slot is free:
+//   (1) own LDS-DMA pieces of chunk g+1 landed (counted vmcnt; chunk g+1 was
+//       staged kSlots-2 seams earlier),
+//   (2) s_barrier: chunk g+1 is published and every wave is past chunk g-1,
+//   (3) stage chunk g+kSlots-1 into chunk g-1's slot.
+NL_HD int dma_outstanding_at_seam(int g) {   // stages issued but not needed yet at E_g
+  const int issued_last = (g + kSlots - 2 < kTotalChunks - 1) ? g + kSlots - 2 : kTotalChunks - 1;
+  return issued_last > g + 1 ? issued_last - (g + 1) : 0;
+}
+__device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
+  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
+  const int g = (n + kPf) / kChunkUnits - 1;
+  NERF_STAMP(cx, 2 + 3 * g);
+  wait_vmcnt(kGldsPerStage * dma_outstanding_at_seam(g));
+  compiler_fence();
+  NERF_STAMP(cx, 3 + 3 * g);
+#if !defined(NERF_ABLATE_BARRIER) && !defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no chunk barrier
+  __builtin_amdgcn_s_barrier();
+#endif
+  compiler_fence();
+  NERF_STAMP(cx, 4 + 3 * g);
+  if (g + kSlots - 1 < kTotalChunks) stage_chunk(cx.blob, g + kSlots - 1, cx.lds, cx.wave_u, cx.lane);
+}
+__device__ __forceinline__ void after_unit(const Ctx&, int) {}
+#else
+__device__ __forceinline__ void seam_before(const Ctx&, int) {}
 // After unit n: when it closes chunk g, (1) this wave's reads of slot g are
 // complete (lgkmcnt(0): the slot is restaged after the barrier), (2) its own
 // pieces of chunk g+2 have landed (counted vmcnt), (3) the barrier publishes
@@ -247,6 +297,7 @@ __device__ __forceinline__ void after_unit(const Ctx& cx, int n) {
   NERF_STAMP(cx, 4 + 3 * g);
   if (g + 1 + kAhead < kTotalChunks) stage_chunk(cx.blob, g + 1 + kAhead, cx.lds, cx.wave_u, cx.lane);
 }
+#endif
 
 template <int L>
 __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)[kCols][16],
@@ -286,6 +337,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int n = N0 + q * KU + u;
+      seam_before(cx, n);
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
 #ifndef NERF_BF16_NO_SCHED_PIN
       // keep the prefetch reads here: left alone, the scheduler sinks them next
@@ -326,8 +378,13 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   NERF_STAMP(cx, 0);
 
   // Kick off the weight stream, then do the per-sample prologue under it.
+#ifndef NERF_BF16_SEAM_OLD
+  constexpr int kPrologueStages = kSlots - 1 < kTotalChunks ? kSlots - 1 : kTotalChunks;
+#else
+  constexpr int kPrologueStages = kAhead;
+#endif
 #pragma unroll
-  for (int g = 0; g < kAhead; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+  for (int g = 0; g < kPrologueStages; ++g) stage_chunk(blob, g, lds, wave_u, lane);
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
 
@@ -352,6 +409,15 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     *(bf16x8*)(de_dst) = pack8(def);
     *(bf16x8*)(de_dst + 1024) = pack8(def + 8);
   }
+#ifndef NERF_BF16_SEAM_OLD
+  // chunk 0 published (later stages may still fly); prime the fragment ring
+  wait_vmcnt(kGldsPerStage * (kPrologueStages - 1));
+  __syncthreads();
+  NERF_STAMP(cx, 1);
+  bf16x8 ra[kRing][2], rb[kRing][kCols];
+#pragma unroll
+  for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+#else
   // chunks 0 and 1 published (later stages may still fly); prime the fragment ring
   wait_vmcnt(kGldsPerStage * (kAhead - 2));
   __syncthreads();
@@ -360,6 +426,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 #pragma unroll
   for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
   stage_chunk(blob, kAhead, lds, wave_u, lane);   // the start of chunk 0
+#endif
 
   f32x16 acc[kCols][8];
   bf16x8 bh[kCols][16];
