@@ -7,12 +7,13 @@
 // bf16 (RNE) at MFMA inputs; accumulation, bias, ReLU, the density/colour heads
 // and everything outside the MLP stay fp32.
 //
-// Geometry: 256-thread workgroups (4 waves, one per SIMD) of 256 samples; a
-// wave owns two 32-sample column tiles, so every A (weight) fragment it reads
-// feeds two MFMAs.  A lane keeps one layer's 2x8 accumulator tiles (256 fp32,
-// AGPRs) and the previous layer as packed bf16 B fragments (128 VGPRs):
-// activations never leave registers (nerf_layout.h).  The position and
-// direction encodings wait in LDS for the layers that take them.
+// Geometry: 512-thread workgroups of 256 samples, 8 waves (two per SIMD), each
+// owning one 32-sample column tile.  A lane keeps one layer's 8 accumulator
+// tiles (128 fp32) and the previous layer as packed bf16 B fragments (64
+// VGPRs): activations never leave registers (nerf_layout.h).  The position and
+// direction encodings wait in LDS for the layers that take them.  (-D
+// NERF_BF16_WAVES=4 builds the one-wave-per-SIMD variant: two column tiles per
+// wave, accumulators in AGPRs.)
 //
 // Quarter schedule.  Each layer is issued in quarters of two output tiles.
 // The previous layer's accumulators are converted to bf16 fragments (ReLU'd),
@@ -23,10 +24,14 @@
 //
 // Weight stream.  The packed blob is a sequence of 2 KiB units (layer, quarter,
 // k-step) cut into 16 KiB chunks.  A 4-slot LDS ring is filled by
-// global_load_lds_dwordx4 (lane-linear 1 KiB pieces) three chunks ahead; one raw
-// s_barrier per chunk publishes the chunk two ahead (counted vmcnt, never 0 in
-// the loop).  Fragments are prefetched two units ahead through a 3-entry
-// register ring, across chunk seams.
+// global_load_lds_dwordx4 (lane-linear 1 KiB pieces, issued from inline asm)
+// three chunks ahead.  One raw s_barrier per chunk, placed where the fragment
+// prefetch first reaches into the next chunk, both publishes that chunk (after
+// a counted vmcnt for this wave's own pieces, never 0 in the loop) and frees
+// the slot of the chunk before, which is restaged right away.  Fragments are
+// prefetched two units ahead through a 3-entry register ring; every LDS read
+// in the loop is inline asm, and each unit waits once, with a compile-time
+// lgkmcnt, for exactly the reads its MFMAs consume.
 #include "nerf_device.h"
 #include "nerf_internal.h"
 
@@ -188,6 +193,10 @@ struct Ctx {
   const char* blob;
   char* lds;
   int wave_u, lane, h;
+  // LDS byte addresses of this lane's 16 B in the ring, in this wave's position /
+  // direction encodings, and of this lane half's bias rows (asm reads add an
+  // immediate offset)
+  unsigned ring_addr, pe_addr, de_addr, bias_addr;
 };
 
 // Tile t of column c of the previous layer -> B fragments 2t, 2t+1 (register
@@ -212,9 +221,72 @@ __device__ __forceinline__ void convert_tile(const f32x16& acc_t, bf16x8& b0, bf
   }
 }
 
+#ifndef NERF_BF16_CC_LDS
+// ---- LDS fragment reads from inline asm with counted waits.  Left to itself
+// hipcc puts an s_waitcnt in front of almost every MFMA (one per fragment);
+// here each unit waits once, for exactly the reads it consumes: everything the
+// loop reads from LDS (fragments, encodings, biases) is issued below, so the
+// count of younger reads is known at compile time.  An asm destination counts
+// as written at the asm statement, so each wait is followed by a
+// sched_barrier that keeps the consuming MFMAs behind it (§5.7 rule 18).
+NL_HD int unit_reads(int n) { return n < 0 || n >= kUnits ? 0 : 2 + (unit_extra(n) != 0 ? kCols : 0); }
+
+// off must fold to a constant in [0, 65536) after unrolling (16-bit offset field)
+__device__ __forceinline__ bf16x8 ds_read_frag(unsigned addr, int off) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  return v;
+}
+__device__ __forceinline__ f32x4 ds_read_f4(unsigned addr, int off) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  return v;
+}
+// s_waitcnt lgkmcnt(k), k a constant after unrolling (gfx9: 4-bit field)
+__device__ __forceinline__ void wait_lgkm(int k) {
+#define NERF_LG(N) else if (k == N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory");
+  if (k <= 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  NERF_LG(1) NERF_LG(2) NERF_LG(3) NERF_LG(4) NERF_LG(5) NERF_LG(6) NERF_LG(7) NERF_LG(8) NERF_LG(9)
+  NERF_LG(10) NERF_LG(11) NERF_LG(12) NERF_LG(13) NERF_LG(14)
+  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#undef NERF_LG
+  __builtin_amdgcn_sched_barrier(0);
+}
+// Issue order per unit body m: [bias reads if m opens a quarter], reads of unit
+// m+kPf, wait, MFMAs of unit m (the prologue issued units 0..kPf-1).
+NL_HD bool unit_opens_quarter(int n) {
+  const int l = unit_layer(n);
+  return (n - bf16_unit_base(l)) % ksteps_bf16(l) == 0;
+}
+constexpr int kBiasReads = 8 * kCols;   // 2 tiles x 4 x 16 B, per column
+NL_HD int bias_reads(int m) { return m >= 0 && m < kUnits && unit_opens_quarter(m) ? kBiasReads : 0; }
+// LDS reads younger than everything unit n consumes, at its wait
+NL_HD int lgkm_for_unit(int n) {
+  if (unit_opens_quarter(n)) return unit_reads(n + kPf);      // this body's bias is the youngest need
+  int c = 0;
+  for (int k = n + 1; k <= n + kPf; ++k) c += unit_reads(k);
+  for (int m = n - kPf + 1; m <= n; ++m) c += bias_reads(m);
+  return c;
+}
+#endif
+
 // Reads of unit n into ring entry n % kRing: two A fragments (output tiles of
 // the unit's quarter) and, for encoding inputs, the two columns' B fragments.
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols]) {
+#ifndef NERF_BF16_CC_LDS
+  static_assert(kSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
+  const int slot_off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes;
+  ra[n % kRing][0] = ds_read_frag(cx.ring_addr, slot_off);
+  ra[n % kRing][1] = ds_read_frag(cx.ring_addr, slot_off + 1024);
+  const int ex = unit_extra(n);
+  if (ex != 0) {
+    const int u = unit_kstep(n) - layer_shape(unit_layer(n)).hidden / 16;
+#pragma unroll
+    for (int c = 0; c < kCols; ++c)
+      rb[n % kRing][c] = ex == kPos ? ds_read_frag(cx.pe_addr, (4 * c + u) * 1024)
+                                    : ds_read_frag(cx.de_addr, (2 * c + u) * 1024);
+  }
+#else
   const char* slot = cx.lds + ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes + cx.lane * 16;
   ra[n % kRing][0] = *(const bf16x8*)(slot);
   ra[n % kRing][1] = *(const bf16x8*)(slot + 1024);
@@ -228,6 +300,7 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
       rb[n % kRing][c] = *(const bf16x8*)(cx.lds + off + cx.lane * 16);
     }
   }
+#endif
 }
 
 // s_waitcnt vmcnt(k) for a k that is a constant only after unrolling.
@@ -310,7 +383,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
   constexpr int N0 = bf16_unit_base(L);
   constexpr bool kConvert = L != L0;          // B fragments come from the previous layer
   constexpr bool kDensity = L == C0;          // ... which, before C0, also feeds the density head
-  const float* prm = (const float*)(cx.lds + kLdsParamOff);
+  [[maybe_unused]] const float* prm = (const float*)(cx.lds + kLdsParamOff);
   if (kConvert) {
     // This wave's reads of the previous layer's last units are issued; the
     // conversion of tiles 0-1 is the only part not hidden behind MFMAs.
@@ -321,6 +394,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
+#ifdef NERF_BF16_CC_LDS
     // bias pre-load of this quarter's two output tiles (both columns)
 #pragma unroll
     for (int o2 = 0; o2 < 2; ++o2) {
@@ -334,11 +408,31 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
           for (int e = 0; e < 4; ++e) acc[c][2 * q + o2][4 * i + e] = b[e];
       }
     }
+#endif
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int n = N0 + q * KU + u;
       seam_before(cx, n);
+#ifndef NERF_BF16_CC_LDS
+      if (u == 0) {
+        // bias pre-load of this quarter's two output tiles, straight into the
+        // accumulators (param blob: [layer][tile][half][16] floats)
+#pragma unroll
+        for (int o2 = 0; o2 < 2; ++o2)
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) {
+            const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
+            const f32x4 b0 = ds_read_f4(cx.bias_addr, off), b1 = ds_read_f4(cx.bias_addr, off + 16);
+            const f32x4 b2 = ds_read_f4(cx.bias_addr, off + 32), b3 = ds_read_f4(cx.bias_addr, off + 48);
+            acc[c][2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                        b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+          }
+      }
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      wait_lgkm(lgkm_for_unit(n));
+#else
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+#endif
 #ifndef NERF_BF16_NO_SCHED_PIN
       // keep the prefetch reads here: left alone, the scheduler sinks them next
       // to their MFMAs and every unit then waits out the LDS latency
@@ -373,7 +467,11 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
-  const Ctx cx{blob, lds, wave_u, lane, h};
+  const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  const Ctx cx{blob, lds, wave_u, lane, h, lds_base + lane * 16,
+               lds_base + kLdsPeOff + wave_u * kCols * 4096 + lane * 16,
+               lds_base + kLdsDeOff + wave_u * kCols * 2048 + lane * 16,
+               lds_base + kLdsParamOff + h * 64};
   const long p0 = (long(blockIdx.x) * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
   NERF_STAMP(cx, 0);
 

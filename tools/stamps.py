@@ -71,8 +71,22 @@ def main():
         per_layer[name] = {"chunks": len(idx), "compute_med": float(np.median(compute[:, :, idx].sum(2))),
                            "wait_med": float(np.median(waits[:, :, idx].sum(2))),
                            "barrier_med": float(np.median(barrier[:, :, idx].sum(2)))}
+    # Skew at the seams: arrival of each wave relative to the block's first
+    # arrival.  Waves w and w+4 share a SIMD (round-robin wave placement).
+    rel = arrive - arrive.min(axis=1, keepdims=True)                  # [blocks, waves, seams]
+    nw = waves.value
+    skew = {"per_wave_mean_late": [float(v) for v in rel.mean(axis=(0, 2))],
+            "spread_med": float(np.median(rel.max(axis=1))),
+            "dma_wait_p50_p90_p99": [float(np.percentile(waits, p)) for p in (50, 90, 99)]}
+    if nw == 8:
+        pair_last = np.maximum(arrive[:, :4], arrive[:, 4:])            # per SIMD: its last wave
+        pair_first = np.minimum(arrive[:, :4], arrive[:, 4:])
+        skew["intra_simd_gap_med"] = float(np.median(pair_last - pair_first))
+        skew["inter_simd_spread_med"] = float(np.median(pair_last.max(axis=1) - pair_last.min(axis=1)))
+        # which wave of a pair is late, as a fraction of seams
+        skew["upper_wave_late_frac"] = float((arrive[:, 4:] > arrive[:, :4]).mean())
     out = {
-        "kernel_ms": ms, "waves": waves.value, "chunks": n_chunks,
+        "kernel_ms": ms, "waves": waves.value, "chunks": n_chunks, "skew": skew,
         "total_med": float(np.median(total)), "prologue_med": float(np.median(prologue)),
         "compute_med": float(np.median(compute.sum(2))), "wait_med": float(np.median(waits.sum(2))),
         "barrier_med": float(np.median(barrier.sum(2))),
