@@ -125,6 +125,28 @@ int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
                 int n_importance, const float* u, int precision, float* rgb_out, float* depth_out,
                 void* stream);
 
+/* nerf_render with the random draws injected per ray (the training-time sampling of
+ * VolumeRenderer, src/utils/rendering.py:36-50 and :79):
+ *   t_rand: device [(row1-row0)*width][n_samples] uniform draws that stratify the
+ *           first-pass samples (rendering.py:42-47); NULL = the uniform table;
+ *   u_rays: device [(row1-row0)*width][n_importance], ascending per ray, replaces the
+ *           shared host u (rendering.py:79 draws one row per ray); NULL = as nerf_render.
+ * nerf_render(...) is nerf_render_sampled(..., t_rand = NULL, u_rays = NULL, ...). */
+int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1,
+                        float focal, float near_, float far_, const float* t_vals, int n_samples,
+                        int n_importance, const float* u, const float* t_rand, const float* u_rays,
+                        int precision, float* rgb_out, float* depth_out, void* stream);
+
+/* Replaces: BaseUnifiedRenderer.sample_points_on_rays (src/benchmark/base_renderer.py:260-281)
+ * and, with t_rand, VolumeRenderer.sample_points_on_rays(perturb=True)
+ * (src/utils/rendering.py:17-52) with torch.rand_like injected.  t_vals: host [n_samples]
+ * linspace table; t_rand: device [n_rays][n_samples] or NULL.  Outputs device: z_out
+ * [n_rays][n_samples]; points_out [n_rays][n_samples][3] = o + d*z (may be NULL, and then
+ * rays_o / rays_d may be NULL too). */
+int nerf_sample_points(nerf_ctx* ctx, const float* rays_o, const float* rays_d, int n_rays,
+                       const float* t_vals, int n_samples, float near_, float far_,
+                       const float* t_rand, float* z_out, float* points_out, void* stream);
+
 /* Per-stage device time of the last nerf_render on this context, from HIP events
  * recorded on the caller's stream when profiling is on.  Stages:
  * 0 rays, 1 coarse MLP, 2 importance, 3 fine MLP, 4 composite. */

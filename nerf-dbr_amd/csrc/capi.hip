@@ -228,6 +228,25 @@ int nerf_importance_sample(const float* z_coarse, int z_ray_stride, const float*
   return NERF_OK;
 }
 
+int nerf_sample_points(nerf_ctx* ctx, const float* rays_o, const float* rays_d, int n_rays, const float* t_vals,
+                       int n_samples, float near_, float far_, const float* t_rand, float* z_out, float* points_out,
+                       void* stream) {
+  if (!ctx) return set_error(NERF_E_INVALID, "null context");
+  if (n_rays < 0 || n_samples <= 0 || n_samples > 1024) return set_error(NERF_E_INVALID, "nerf_sample_points: bad sizes");
+  if (n_rays == 0) return NERF_OK;
+  if (!t_vals || !z_out || (points_out && (!rays_o || !rays_d)))
+    return set_error(NERF_E_INVALID, "nerf_sample_points: null pointer");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = grow(ctx->zbuf, ctx->z_cap, 1024, "z");
+  if (rc != NERF_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(s));   // host_stage may still feed a previous copy
+  nerf_uniform_z(t_vals, n_samples, near_, far_, ctx->host_stage);
+  HIP_TRY(hipMemcpyAsync(ctx->zbuf, ctx->host_stage, sizeof(float) * n_samples, hipMemcpyHostToDevice, s));
+  HIP_TRY(launch_sample(ctx->zbuf, t_rand, n_rays, n_samples, rays_o, rays_d, z_out, points_out, s));
+  return NERF_OK;
+}
+
 int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable) {
   if (!ctx) return set_error(NERF_E_INVALID, "null context");
   ctx->profiling = enable != 0;
@@ -248,6 +267,14 @@ int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out) {
 int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal, float near_,
                 float far_, const float* t_vals, int n_samples, int n_importance, const float* u, int precision,
                 float* rgb_out, float* depth_out, void* stream) {
+  return nerf_render_sampled(ctx, c2w, width, height, row0, row1, focal, near_, far_, t_vals, n_samples, n_importance,
+                             u, nullptr, nullptr, precision, rgb_out, depth_out, stream);
+}
+
+int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal,
+                        float near_, float far_, const float* t_vals, int n_samples, int n_importance, const float* u,
+                        const float* t_rand, const float* u_rays, int precision, float* rgb_out, float* depth_out,
+                        void* stream) {
   const int net_main = NERF_NET_FINE;
   int rc = check_net(ctx, net_main, precision);
   if (rc != NERF_OK) return rc;
@@ -275,13 +302,16 @@ int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
 
   if ((rc = grow(ctx->rays, ctx->rays_cap, size_t(n_rays) * 6, "rays")) != NERF_OK) return rc;
   if ((rc = grow(ctx->mlp_out, ctx->mlp_cap, size_t(n_rays) * n_fine * 4, "mlp_out")) != NERF_OK) return rc;
-  const size_t zfloats = 1024 + (n_importance > 0 ? size_t(n_rays) * n_fine : 0);
+  // z buffer: [table 1024][stratified first-pass z, R x S][fine z, R x (S+N)]
+  const size_t strat_floats = t_rand ? size_t(n_rays) * n_samples : 0;
+  const size_t zfloats = 1024 + strat_floats + (n_importance > 0 ? size_t(n_rays) * n_fine : 0);
   if ((rc = grow(ctx->zbuf, ctx->z_cap, zfloats, "z")) != NERF_OK) return rc;
   const size_t wfloats = 1024 + (n_importance > 0 ? size_t(n_rays) * n_samples : 0);
   if ((rc = grow(ctx->wbuf, ctx->w_cap, wfloats, "weights")) != NERF_OK) return rc;
 
   float* d_ztab = ctx->zbuf;
-  float* d_zfine = ctx->zbuf + 1024;
+  float* d_zstrat = ctx->zbuf + 1024;
+  float* d_zfine = ctx->zbuf + 1024 + strat_floats;
   float* d_u = ctx->wbuf;
   float* d_w = ctx->wbuf + 1024;
   float* rays_o = ctx->rays;
@@ -296,19 +326,28 @@ int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
   };
   if ((rc = mark(0)) != NERF_OK) return rc;
   HIP_TRY(launch_generate_rays(c2w, width, height, row0, row1, focal, rays_o, rays_d, s));
+  // first-pass samples: the shared table, or stratified per ray (rendering.py:42-47)
+  const float* z_first = d_ztab;
+  int z_first_stride = 0;
+  if (t_rand) {
+    HIP_TRY(launch_sample(d_ztab, t_rand, int(n_rays), n_samples, nullptr, nullptr, d_zstrat, nullptr, s));
+    z_first = d_zstrat;
+    z_first_stride = n_samples;
+  }
   ctx->stage_ran[0] = true;
   if ((rc = mark(1)) != NERF_OK) return rc;
-  const float* z_main = d_ztab;
-  int z_stride = 0;
+  const float* z_main = z_first;
+  int z_stride = z_first_stride;
   if (n_importance > 0) {
-    SampleSrc src{rays_o, rays_d, d_ztab, 0, n_samples, nullptr, nullptr};
+    SampleSrc src{rays_o, rays_d, z_first, z_first_stride, n_samples, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s));
     ctx->stage_ran[1] = true;
     if ((rc = mark(2)) != NERF_OK) return rc;
     // coarse weights only (the coarse image itself is not an output of render_image)
-    HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, d_ztab, 0, rays_d, int(n_rays), n_samples,
-                             rgb_out, depth_out, nullptr, d_w, s));
-    HIP_TRY(launch_importance(d_ztab, 0, d_w, d_u, 0, int(n_rays), n_samples, n_importance, d_zfine, s));
+    HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_first, z_first_stride, rays_d, int(n_rays),
+                             n_samples, rgb_out, depth_out, nullptr, d_w, s));
+    HIP_TRY(launch_importance(z_first, z_first_stride, d_w, u_rays ? u_rays : d_u, u_rays ? n_importance : 0,
+                              int(n_rays), n_samples, n_importance, d_zfine, s));
     ctx->stage_ran[2] = true;
     z_main = d_zfine;
     z_stride = n_fine;

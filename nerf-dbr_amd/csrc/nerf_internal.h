@@ -21,6 +21,8 @@ hipError_t launch_composite(const float* sigma, int sigma_stride, const float* r
                             const float* z, int z_ray_stride, const float* rays_d, int n_rays, int n_samples,
                             float* rgb_out, float* depth_out, float* acc_out, float* weights_out,
                             hipStream_t stream);
+hipError_t launch_sample(const float* z_tab, const float* t_rand, int n_rays, int n_samples, const float* rays_o,
+                         const float* rays_d, float* z_out, float* points_out, hipStream_t stream);
 hipError_t launch_importance(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
                              int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine,
                              hipStream_t stream);

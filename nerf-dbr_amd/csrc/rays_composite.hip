@@ -134,7 +134,46 @@ __global__ void importance_kernel(const float* __restrict__ z_coarse, int z_ray_
   while (ic < n_coarse) out[o++] = zr[ic++];
 }
 
+// Sample depths and points, one thread per (ray, sample).
+// Uniform (BaseUnifiedRenderer.sample_points_on_rays, base_renderer.py:260-281):
+//   z = table[s] (near*(1-t)+far*t, built on the host bit-exactly).
+// Stratified (VolumeRenderer.sample_points_on_rays perturb=True, rendering.py:42-47,
+// with torch.rand_like injected as t_rand [n_rays][S]):
+//   mids_j = 0.5*(z[j+1]+z[j]); lower = [z0, mids]; upper = [mids, z_{S-1}];
+//   z' = lower + (upper-lower)*t_rand.
+// Points (rendering.py:50 / base_renderer.py:279): o + d*z, multiply then add.
+__global__ void sample_kernel(const float* __restrict__ z_tab, const float* __restrict__ t_rand, int n_samples,
+                              long n, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                              float* __restrict__ z_out, float* __restrict__ points_out) {
+  const long i = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = int(i % n_samples);
+  const long r = i / n_samples;
+  float z = z_tab[s];
+  if (t_rand) {
+    const float lower = s == 0 ? z_tab[0] : __fmul_rn(0.5f, __fadd_rn(z_tab[s], z_tab[s - 1]));
+    const float upper = s == n_samples - 1 ? z_tab[s] : __fmul_rn(0.5f, __fadd_rn(z_tab[s + 1], z_tab[s]));
+    z = __fadd_rn(lower, __fmul_rn(__fsub_rn(upper, lower), t_rand[i]));
+  }
+  z_out[i] = z;
+  if (points_out) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) points_out[3 * i + c] = __fadd_rn(rays_o[3 * r + c], __fmul_rn(rays_d[3 * r + c], z));
+  }
+}
+
 }  // namespace
+
+hipError_t launch_sample(const float* z_tab, const float* t_rand, int n_rays, int n_samples, const float* rays_o,
+                         const float* rays_d, float* z_out, float* points_out, hipStream_t stream) {
+  const long n = long(n_rays) * n_samples;
+  if (n <= 0) return hipSuccess;
+  const int threads = 256;
+  const dim3 grid{unsigned((n + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  hipLaunchKernelGGL(sample_kernel, grid, block, 0, stream, z_tab, t_rand, n_samples, n, rays_o, rays_d, z_out,
+                     points_out);
+  return hipGetLastError();
+}
 
 hipError_t launch_generate_rays(const float* c2w, int width, int height, int row0, int row1, float focal,
                                 float* rays_o, float* rays_d, hipStream_t stream) {

@@ -97,8 +97,12 @@ class MI355XRenderer(BaseUnifiedRenderer):
         return self._u_cache[n]
 
     def render_rows(self, camera_pose, resolution: Tuple[int, int], samples_per_ray: int, row0: int, row1: int,
-                    rgb_out=None, depth_out=None):
-        """Rows [row0, row1) of the image: rgb [rows, W, 3], depth [rows, W] (device tensors)."""
+                    rgb_out=None, depth_out=None, t_rand=None, u=None):
+        """Rows [row0, row1) of the image: rgb [rows, W, 3], depth [rows, W] (device tensors).
+
+        Optional per-ray draws (training-style sampling, rendering.py:36-50 / :79):
+        ``t_rand`` [rows*W, S] stratifies the first-pass samples; ``u`` [rows*W, n_importance]
+        (ascending per ray) replaces the deterministic linspace importance draw."""
         import torch
 
         width, height = resolution
@@ -108,11 +112,13 @@ class MI355XRenderer(BaseUnifiedRenderer):
             rgb_out = torch.empty(rows, width, 3, dtype=torch.float32, device=dev)
         if depth_out is None:
             depth_out = torch.empty(rows, width, dtype=torch.float32, device=dev)
-        u = self._u(self.n_importance) if self.n_importance else None
+        u_shared = self._u(self.n_importance) if self.n_importance else None
+        tr = None if t_rand is None else t_rand.to(dev, torch.float32).reshape(rows * width, -1).contiguous()
+        ur = None if u is None else u.to(dev, torch.float32).reshape(rows * width, -1).contiguous()
         with torch.cuda.device(self.device_index):
             self.hip.render(_pose_np(camera_pose), width, height, row0, row1, self.focal, self.near, self.far,
-                            t_vals(samples_per_ray), self.n_importance, u, rt.PRECISIONS[self.precision],
-                            rgb_out, depth_out)
+                            t_vals(samples_per_ray), self.n_importance, u_shared, rt.PRECISIONS[self.precision],
+                            rgb_out, depth_out, t_rand=tr, u_rays=ur)
         return rgb_out, depth_out
 
     def render_image(self, camera_pose, resolution: Tuple[int, int], samples_per_ray: int = 64):
@@ -131,13 +137,23 @@ class MI355XRenderer(BaseUnifiedRenderer):
             self.hip.generate_rays(_pose_np(camera_pose), width, height, 0, height, focal, o, d)
         return o, d
 
-    def sample_points_on_rays(self, rays_o, rays_d, n_samples: int = 64):
-        """base_renderer.py:260-281 as an API helper (the render path fuses it into the MLP kernel)."""
+    def sample_points_on_rays(self, rays_o, rays_d, n_samples: int = 64, t_rand=None):
+        """base_renderer.py:260-281 -> (points [N,S,3], z [N,S]) on the device (sample_kernel;
+        the render path fuses this step into the MLP kernel).  With ``t_rand`` [N,S] (uniform
+        draws in [0,1)) the samples are stratified as VolumeRenderer.sample_points_on_rays
+        (perturb=True) does (rendering.py:42-47) with its torch.rand_like injected."""
         import torch
 
-        z_row = torch.from_numpy(rt.uniform_z(t_vals(n_samples), self.near, self.far)).to(rays_o.device)
-        z = z_row.expand(rays_o.shape[0], n_samples)
-        return rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None], z
+        dev = torch.device("cuda", self.device_index)
+        o = rays_o.to(dev, torch.float32).reshape(-1, 3).contiguous()
+        d = rays_d.to(dev, torch.float32).reshape(-1, 3).contiguous()
+        n = o.shape[0]
+        tr = None if t_rand is None else t_rand.to(dev, torch.float32).reshape(n, n_samples).contiguous()
+        z = torch.empty(n, n_samples, dtype=torch.float32, device=dev)
+        pts = torch.empty(n, n_samples, 3, dtype=torch.float32, device=dev)
+        with torch.cuda.device(self.device_index):
+            self.hip.sample_points(o, d, t_vals(n_samples), self.near, self.far, z, pts, tr)
+        return pts, z
 
     def query_nerf_networks(self, positions, directions, use_fine: bool = True):
         import torch

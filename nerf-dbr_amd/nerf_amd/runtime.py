@@ -54,6 +54,10 @@ SIGNATURES = {
     "nerf_importance_sample": (_c.c_int, [_P, _c.c_int, _P, _P, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P]),
     "nerf_render": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float,
                                _c.c_float, _FP, _c.c_int, _c.c_int, _FP, _c.c_int, _P, _P, _P]),
+    "nerf_render_sampled": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float,
+                                       _c.c_float, _FP, _c.c_int, _c.c_int, _FP, _P, _P, _c.c_int, _P, _P, _P]),
+    "nerf_sample_points": (_c.c_int, [_P, _P, _P, _c.c_int, _FP, _c.c_int, _c.c_float, _c.c_float, _P, _P, _P,
+                                      _P]),
     "nerf_ctx_set_profiling": (_c.c_int, [_P, _c.c_int]),
     "nerf_ctx_stage_ms": (_c.c_int, [_P, _FP]),
 }
@@ -134,6 +138,12 @@ def _ptr(t) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
+def torch_float32():
+    import torch
+
+    return torch.float32
+
+
 def _stream(stream) -> int:
     import torch
 
@@ -205,13 +215,30 @@ class Device:
 
     def render(self, c2w: np.ndarray, width: int, height: int, row0: int, row1: int, focal: float, near: float,
                far: float, t_vals: np.ndarray, n_importance: int, u: Optional[np.ndarray], precision: int,
-               rgb_out, depth_out, stream=None) -> None:
+               rgb_out, depth_out, stream=None, t_rand=None, u_rays=None) -> None:
+        """t_rand [rays, S] / u_rays [rays, N]: optional per-ray draws (device tensors)."""
         pose = np.ascontiguousarray(np.asarray(c2w, dtype=np.float32).reshape(4, 4))
         t = np.ascontiguousarray(t_vals, dtype=np.float32)
         uu = None if u is None else np.ascontiguousarray(u, dtype=np.float32)
-        _check(self.lib.nerf_render(self._ctx, _fptr(pose), width, height, row0, row1, focal, near, far, _fptr(t),
-                                    t.size, n_importance, None if uu is None else _fptr(uu), precision,
-                                    _ptr(rgb_out), _ptr(depth_out), _stream(stream)))
+        n_rays = (row1 - row0) * width
+        if t_rand is not None and tuple(t_rand.shape) != (n_rays, t.size):
+            raise ValueError(f"t_rand must be [{n_rays}, {t.size}], got {tuple(t_rand.shape)}")
+        if u_rays is not None and tuple(u_rays.shape) != (n_rays, n_importance):
+            raise ValueError(f"u_rays must be [{n_rays}, {n_importance}], got {tuple(u_rays.shape)}")
+        for name, a in (("t_rand", t_rand), ("u_rays", u_rays)):
+            if a is not None and not (a.is_cuda and a.dtype == torch_float32() and a.is_contiguous()):
+                raise ValueError(f"{name} must be a contiguous float32 device tensor")
+        _check(self.lib.nerf_render_sampled(self._ctx, _fptr(pose), width, height, row0, row1, focal, near, far,
+                                            _fptr(t), t.size, n_importance, None if uu is None else _fptr(uu),
+                                            _ptr(t_rand), _ptr(u_rays), precision, _ptr(rgb_out), _ptr(depth_out),
+                                            _stream(stream)))
+
+    def sample_points(self, rays_o, rays_d, t_vals: np.ndarray, near: float, far: float, z_out, points_out=None,
+                      t_rand=None, stream=None) -> None:
+        t = np.ascontiguousarray(t_vals, dtype=np.float32)
+        n = z_out.shape[0]
+        _check(self.lib.nerf_sample_points(self._ctx, _ptr(rays_o), _ptr(rays_d), n, _fptr(t), t.size, near, far,
+                                           _ptr(t_rand), _ptr(z_out), _ptr(points_out), _stream(stream)))
 
     def set_profiling(self, enable: bool) -> None:
         _check(self.lib.nerf_ctx_set_profiling(self._ctx, 1 if enable else 0))

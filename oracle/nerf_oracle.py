@@ -172,15 +172,20 @@ def default_u(n_rays: int, n_importance: int) -> torch.Tensor:
 
 # ---------------------------------------------------------- a7 full image --
 def render_rays(net: Net, rays_o, rays_d, n_samples: int, chunk: int = CHUNK,
-                near: float = NEAR, far: float = FAR):
-    """_render_ray_chunk (pytorch_renderers.py:156-170) over 512-ray chunks."""
+                near: float = NEAR, far: float = FAR, t_rand=None):
+    """_render_ray_chunk (pytorch_renderers.py:156-170) over 512-ray chunks.  With
+    t_rand [N, S] the samples are stratified (rendering.py:42-47, draw injected)."""
     rays_o, rays_d = _t(rays_o).reshape(-1, 3), _t(rays_d).reshape(-1, 3)
     z_row = uniform_z(n_samples, near, far)
+    if t_rand is not None:
+        t_rand = _t(t_rand).reshape(rays_o.shape[0], n_samples)
     rgbs, depths = [], []
     with torch.no_grad():
         for c in range(0, rays_o.shape[0], chunk):
             o, d = rays_o[c:c + chunk], rays_d[c:c + chunk]
             z = z_row.expand(o.shape[0], n_samples)
+            if t_rand is not None:
+                z = stratified_z(z_row, t_rand[c:c + chunk])
             pts = sample_points(o, d, z)
             dirs = d[:, None, :].expand_as(pts).reshape(-1, 3)
             sigma, rgb = nerf_forward(net, pts.reshape(-1, 3), dirs)
@@ -193,19 +198,20 @@ def render_rays(net: Net, rays_o, rays_d, n_samples: int, chunk: int = CHUNK,
 
 
 def render_image(net: Net, c2w, resolution: Tuple[int, int], n_samples: int = 64,
-                 rows: Optional[Tuple[int, int]] = None):
-    """PyTorchCPURenderer.render_image (pytorch_renderers.py:127-154); optional row band."""
+                 rows: Optional[Tuple[int, int]] = None, t_rand=None):
+    """PyTorchCPURenderer.render_image (pytorch_renderers.py:127-154); optional row band
+    and optional stratification draws t_rand [rows*W, S]."""
     width, height = resolution
     rays_o, rays_d = generate_rays(c2w, width, height)
     r0, r1 = rows if rows is not None else (0, height)
-    rgb, depth = render_rays(net, rays_o[r0:r1], rays_d[r0:r1], n_samples)
+    rgb, depth = render_rays(net, rays_o[r0:r1], rays_d[r0:r1], n_samples, t_rand=t_rand)
     return rgb.reshape(r1 - r0, width, 3), depth.reshape(r1 - r0, width)
 
 
 def render_image_hierarchical(coarse: Net, fine: Net, c2w, resolution: Tuple[int, int],
                               n_coarse: int = 64, n_importance: int = 128,
                               u: Optional[torch.Tensor] = None, chunk: int = CHUNK,
-                              rows: Optional[Tuple[int, int]] = None):
+                              rows: Optional[Tuple[int, int]] = None, t_rand=None):
     """Build-defined 64+128 hierarchical render: coarse net on the
     uniform samples, importance samples from its weights, fine net on the sorted union."""
     width, height = resolution
@@ -217,12 +223,16 @@ def render_image_hierarchical(coarse: Net, fine: Net, c2w, resolution: Tuple[int
         u = default_u(n, n_importance)
     u = _t(u)
     z_row = uniform_z(n_coarse)
+    if t_rand is not None:
+        t_rand = _t(t_rand).reshape(n, n_coarse)
     rgbs, depths = [], []
     with torch.no_grad():
         for c in range(0, n, chunk):
             o, d = rays_o[c:c + chunk], rays_d[c:c + chunk]
             m = o.shape[0]
             zc = z_row.expand(m, n_coarse)
+            if t_rand is not None:     # stratified coarse samples (rendering.py:42-47)
+                zc = stratified_z(z_row, t_rand[c:c + chunk])
             pts = sample_points(o, d, zc)
             dirs = d[:, None, :].expand_as(pts).reshape(-1, 3)
             s, r = nerf_forward(coarse, pts.reshape(-1, 3), dirs)

@@ -214,3 +214,88 @@ def test_edge_shapes_vs_oracle(r32, ckpt, res, s):
     rgb, depth = r32.render_image(pose, res, s)
     ref_rgb, ref_depth = O.render_image(O.Net(f), pose, res, s)
     assert maxabs(rgb, ref_rgb.numpy()) < TOL_RENDER and maxabs(depth, ref_depth.numpy()) < TOL_RENDER
+
+
+# ------------------------------------------------ stratified sampling (a2s) --
+def test_sample_points_bit_exact(r32, golden):
+    """sample_kernel vs the reference's own VolumeRenderer.sample_points_on_rays
+    (perturb=True, captured t_rand) and the benchmark's uniform sampler."""
+    from oracle import nerf_oracle as O
+
+    g = golden("stratified")
+    o, d = torch.from_numpy(g["rays_o"]), torch.from_numpy(g["rays_d"])
+    s = g["t_rand"].shape[1]
+    pts, z = r32.sample_points_on_rays(o, d, s, t_rand=torch.from_numpy(g["t_rand"]))
+    assert np.array_equal(z.cpu().numpy(), g["z"])
+    assert np.array_equal(pts.cpu().numpy(), g["pts"])
+    pts, z = r32.sample_points_on_rays(o, d, s)
+    z_ref = O.uniform_z(s).expand(o.shape[0], s)
+    assert np.array_equal(z.cpu().numpy(), z_ref.numpy())
+    assert np.array_equal(pts.cpu().numpy(), O.sample_points(o, d, z_ref).numpy())
+    for n_s in (1, 2):                          # degenerate strata
+        t = torch.rand(o.shape[0], n_s)
+        _, z = r32.sample_points_on_rays(o, d, n_s, t_rand=t)
+        assert np.array_equal(z.cpu().numpy(), O.stratified_z(O.uniform_z(n_s), t).numpy())
+
+
+def test_render_stratified_fp32_vs_oracle(r32):
+    from oracle import nerf_oracle as O
+
+    _, f = W.synthetic_models(0)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
+    gen = torch.Generator().manual_seed(0)
+    w, h, s = 64, 48, 32
+    t_rand = torch.rand(w * h, s, generator=gen)
+    rgb, depth = r32.render_rows(pose, (w, h), s, 0, h, t_rand=t_rand)
+    ref_rgb, ref_depth = O.render_image(O.Net(f), pose, (w, h), s, t_rand=t_rand)
+    er, ed = maxabs(rgb, ref_rgb.numpy()), maxabs(depth, ref_depth.numpy())
+    print(f"stratified 64x48x32: rgb {er:.3e} depth {ed:.3e}")
+    assert er < TOL_RENDER and ed < TOL_RENDER
+    # a row band draws its own rows' t_rand
+    rgb_b, _ = r32.render_rows(pose, (w, h), s, 10, 20, t_rand=t_rand[10 * w:20 * w])
+    assert torch.equal(rgb_b, rgb[10:20])
+
+
+def test_render_stratified_hierarchical_stagewise(r32):
+    """Stratified coarse samples + per-ray random u: the importance stage is bit-exact
+    and the fine image within TOL_RENDER when fed the oracle's coarse weights."""
+    from oracle import nerf_oracle as O
+
+    c, _ = W.synthetic_models(0)
+    coarse = O.Net(c)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
+    o, d = O.generate_rays(pose, 32, 16)
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    n, nc, ni = o.shape[0], 64, 128
+    gen = torch.Generator().manual_seed(1)
+    t_rand = torch.rand(n, nc, generator=gen)
+    u = torch.sort(torch.rand(n, ni, generator=gen), -1).values
+    zc = O.stratified_z(O.uniform_z(nc), t_rand)
+    _, zc_gpu = r32.sample_points_on_rays(o, d, nc, t_rand=t_rand)
+    assert np.array_equal(zc_gpu.cpu().numpy(), zc.numpy())
+    pts = O.sample_points(o, d, zc)
+    s_, c_ = O.nerf_forward(coarse, pts.reshape(-1, 3), d[:, None].expand_as(pts).reshape(-1, 3))
+    _, _, _, w_ref = O.composite(s_.reshape(n, nc, 1), c_.reshape(n, nc, 3), zc, d, True)
+    _, _, _, w_gpu = r32.render_rays_z(o, d, zc, use_fine=False, with_weights=True)
+    assert maxabs(w_gpu, w_ref.numpy()) < 1e-4
+    zf_gpu = r32.importance_sample(zc, w_ref, u.contiguous())
+    assert np.array_equal(zf_gpu.cpu().numpy(), O.fine_z(zc, w_ref, u).numpy())
+
+
+def test_render_stratified_hierarchical_end_to_end(ckpt):
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+    from oracle import nerf_oracle as O
+
+    r = MI355XRenderer("fp32", n_importance=64)
+    r.setup(ckpt)
+    c, f = W.synthetic_models(0)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][0])
+    w, h, nc, ni = 32, 24, 32, 64
+    gen = torch.Generator().manual_seed(2)
+    t_rand = torch.rand(w * h, nc, generator=gen)
+    u = torch.sort(torch.rand(w * h, ni, generator=gen), -1).values
+    rgb, depth = r.render_rows(pose, (w, h), nc, 0, h, t_rand=t_rand, u=u)
+    ref_rgb, ref_depth = O.render_image_hierarchical(O.Net(c), O.Net(f), pose, (w, h), nc, ni, u=u, t_rand=t_rand)
+    er, ed = maxabs(rgb, ref_rgb.numpy()), maxabs(depth, ref_depth.numpy())
+    print(f"stratified hierarchical end-to-end {w}x{h} {nc}+{ni}: rgb {er:.3e} depth {ed:.3e}")
+    assert er < 2e-2 and ed < 2e-2
