@@ -27,7 +27,7 @@ for _p in (REPO, os.path.join(REPO, "nerf-dbr_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 METRIC = "rays/sec at 800x600x128spp (render_image, fine net, uniform samples)"
 
 
@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--precision", choices=["bf16", "fp32", "fp8"], default="bf16")
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--spp", type=int, default=128)
@@ -143,15 +143,16 @@ def main():
     peak = PEAK_TFLOPS[args.precision]
 
     extra = {}
-    if rank == 0 and args.precision == "bf16" and not args.no_error_check:
-        # bf16 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
+    if rank == 0 and args.precision != "fp32" and not args.no_error_check:
+        # bf16 / fp8 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
         ref = MI355XRenderer("fp32", device_index=local)
         ref.setup(ckpt)
         a0, a1 = height // 2 - 8, height // 2 + 8
         rgb32, d32 = ref.render_rows(pose, (width, height), spp, a0, a1)
-        rgb16, d16 = r.render_rows(pose, (width, height), spp, a0, a1)
-        extra["bf16_vs_fp32_rgb_max_abs"] = float((rgb16 - rgb32).abs().max())
-        extra["bf16_vs_fp32_depth_max_abs"] = float((d16 - d32).abs().max())
+        rgb_lp, d_lp = r.render_rows(pose, (width, height), spp, a0, a1)
+        extra[f"{args.precision}_vs_fp32_rgb_max_abs"] = float((rgb_lp - rgb32).abs().max())
+        extra[f"{args.precision}_vs_fp32_rgb_mean_abs"] = float((rgb_lp - rgb32).abs().mean())
+        extra[f"{args.precision}_vs_fp32_depth_max_abs"] = float((d_lp - d32).abs().max())
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         ref.render_rows(pose, (width, height), spp, 0, height)

@@ -38,6 +38,10 @@ enum nerf_status {
 enum nerf_precision {
   NERF_FP32 = 0, /* f32-in MFMA (v_mfma_f32_32x32x2_f32); the parity path   */
   NERF_BF16 = 1, /* bf16-in MFMA (v_mfma_f32_32x32x16_bf16), f32 accumulate */
+  NERF_FP8 = 2,  /* e4m3 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4): per-row weight
+                    scales, per-sample activation scales, f32 accumulate; the
+                    compressed-weights path (config 5; the reference's int8
+                    CompressedNeRFRenderer, src/benchmark/compressed_renderer.py) */
 };
 
 enum nerf_net { NERF_NET_COARSE = 0, NERF_NET_FINE = 1 };
@@ -69,6 +73,13 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
 void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob);
 int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob, uint16_t* bf16_blob,
                       float* param_blob);
+
+/* Pure host helpers for the fp8 path: the packed e4m3 blob (fragments + per-row
+ * E8M0 weight scales) the fp8 kernel reads, and the f32 -> e4m3fn (OCP) rounding
+ * it uses (round to nearest even; inputs must be within +-448). */
+size_t nerf_fp8_blob_bytes(void);
+int nerf_pack_weights_fp8(const float* const* params, int n_params, uint8_t* blob);
+void nerf_f32_to_e4m3(const float* x, int n, uint8_t* out);
 
 /* Pure host helper: z = near*(1-t) + far*t in fp32, operation for operation
  * (src/benchmark/base_renderer.py:274-275). */

@@ -33,6 +33,7 @@ using namespace nerf;
 struct NetDev {
   float* f32 = nullptr;
   void* bf16 = nullptr;
+  void* fp8 = nullptr;      // e4m3 fragments + E8M0 row scales (nerf_layout.h)
   float* params = nullptr;
   bool loaded = false;
 };
@@ -73,7 +74,8 @@ int grow(T*& p, size_t& cap, size_t need, const char* what) {
 int check_net(nerf_ctx* ctx, int net, int precision) {
   if (!ctx) return set_error(NERF_E_INVALID, "null context");
   if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
-  if (precision != NERF_FP32 && precision != NERF_BF16) return set_error(NERF_E_INVALID, "bad precision %d", precision);
+  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8)
+    return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (!ctx->net[net].loaded) return set_error(NERF_E_NO_WEIGHTS, "%s network not loaded", net ? "fine" : "coarse");
   return NERF_OK;
 }
@@ -93,6 +95,7 @@ hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, 
                    hipStream_t s) {
   const NetDev& nd = ctx->net[net];
   if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s);
+  if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
 }
 
@@ -138,6 +141,7 @@ void nerf_ctx_destroy(nerf_ctx* ctx) {
   for (auto& nd : ctx->net) {
     if (nd.f32) (void)hipFree(nd.f32);
     if (nd.bf16) (void)hipFree(nd.bf16);
+    if (nd.fp8) (void)hipFree(nd.fp8);
     if (nd.params) (void)hipFree(nd.params);
   }
   for (float* p : {ctx->rays, ctx->mlp_out, ctx->zbuf, ctx->wbuf})
@@ -157,11 +161,16 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
   std::vector<uint16_t> bf(nbf16 / 2);
   int rc = nerf_pack_weights(params, n_params, f32.data(), bf.data(), prm.data());
   if (rc != NERF_OK) return rc;
+  const size_t nfp8 = nerf_fp8_blob_bytes();
+  std::vector<uint8_t> f8(nfp8);
+  if ((rc = nerf_pack_weights_fp8(params, n_params, f8.data())) != NERF_OK) return rc;
   DeviceGuard g(ctx->device);
   NetDev& nd = ctx->net[net];
   if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
   if (!nd.bf16) HIP_TRY(hipMalloc(&nd.bf16, nbf16));
   if (!nd.params) HIP_TRY(hipMalloc((void**)&nd.params, nprm));
+  if (!nd.fp8) HIP_TRY(hipMalloc(&nd.fp8, nfp8));
+  HIP_TRY(hipMemcpy(nd.fp8, f8.data(), nfp8, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.f32, f32.data(), nf32, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.bf16, bf.data(), nbf16, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));

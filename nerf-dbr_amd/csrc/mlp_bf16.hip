@@ -32,6 +32,7 @@
 // prefetched two units ahead through a 3-entry register ring; every LDS read
 // in the loop is inline asm, and each unit waits once, with a compile-time
 // lgkmcnt, for exactly the reads its MFMAs consume.
+#include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
 
@@ -116,28 +117,12 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
     __builtin_amdgcn_global_load_lds((const void*)(src + i * kThreads * 16), (lds_void*)(dst + i * kThreads * 16),
                                      16, 0, 0);
 #else
-    // Issued from inline asm: when hipcc sees an LDS-DMA in a function it stops
-    // counting LDS waits and emits lgkmcnt(0) before every fragment use.  The DMA
-    // completion is tracked by hand (counted vmcnt + barrier at each seam); an asm
-    // VMEM op can only make hipcc's own vmcnt waits stricter, never looser.
-    // M0 (the LDS base) is set and restored inside the statement (§5.7).
-    unsigned keep;
-    const unsigned lds_addr = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(dst + i * kThreads * 16));
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(src + i * kThreads * 16), "s"(lds_addr)
-        : "memory");
+    // issued from inline asm (nerf_asm.h): the builtin makes hipcc emit lgkmcnt(0)
+    // before every fragment use; completion is tracked by counted vmcnt + barrier
+    lds_dma_16(src + i * kThreads * 16, lds_addr(dst + i * kThreads * 16));
 #endif
   }
 }
-
-__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
 __device__ __forceinline__ bf16x8 pack8(const float* v) {
   bf16x8 r;
@@ -231,27 +216,6 @@ __device__ __forceinline__ void convert_tile(const f32x16& acc_t, bf16x8& b0, bf
 // sched_barrier that keeps the consuming MFMAs behind it (§5.7 rule 18).
 NL_HD int unit_reads(int n) { return n < 0 || n >= kUnits ? 0 : 2 + (unit_extra(n) != 0 ? kCols : 0); }
 
-// off must fold to a constant in [0, 65536) after unrolling (16-bit offset field)
-__device__ __forceinline__ bf16x8 ds_read_frag(unsigned addr, int off) {
-  bf16x8 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
-  return v;
-}
-__device__ __forceinline__ f32x4 ds_read_f4(unsigned addr, int off) {
-  f32x4 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
-  return v;
-}
-// s_waitcnt lgkmcnt(k), k a constant after unrolling (gfx9: 4-bit field)
-__device__ __forceinline__ void wait_lgkm(int k) {
-#define NERF_LG(N) else if (k == N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory");
-  if (k <= 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  NERF_LG(1) NERF_LG(2) NERF_LG(3) NERF_LG(4) NERF_LG(5) NERF_LG(6) NERF_LG(7) NERF_LG(8) NERF_LG(9)
-  NERF_LG(10) NERF_LG(11) NERF_LG(12) NERF_LG(13) NERF_LG(14)
-  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#undef NERF_LG
-  __builtin_amdgcn_sched_barrier(0);
-}
 // Issue order per unit body m: [bias reads if m opens a quarter], reads of unit
 // m+kPf, wait, MFMAs of unit m (the prologue issued units 0..kPf-1).
 NL_HD bool unit_opens_quarter(int n) {
@@ -276,15 +240,15 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
 #ifndef NERF_BF16_CC_LDS
   static_assert(kSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
   const int slot_off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes;
-  ra[n % kRing][0] = ds_read_frag(cx.ring_addr, slot_off);
-  ra[n % kRing][1] = ds_read_frag(cx.ring_addr, slot_off + 1024);
+  ra[n % kRing][0] = ds_read_b128<bf16x8>(cx.ring_addr, slot_off);
+  ra[n % kRing][1] = ds_read_b128<bf16x8>(cx.ring_addr, slot_off + 1024);
   const int ex = unit_extra(n);
   if (ex != 0) {
     const int u = unit_kstep(n) - layer_shape(unit_layer(n)).hidden / 16;
 #pragma unroll
     for (int c = 0; c < kCols; ++c)
-      rb[n % kRing][c] = ex == kPos ? ds_read_frag(cx.pe_addr, (4 * c + u) * 1024)
-                                    : ds_read_frag(cx.de_addr, (2 * c + u) * 1024);
+      rb[n % kRing][c] = ex == kPos ? ds_read_b128<bf16x8>(cx.pe_addr, (4 * c + u) * 1024)
+                                    : ds_read_b128<bf16x8>(cx.de_addr, (2 * c + u) * 1024);
   }
 #else
   const char* slot = cx.lds + ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes + cx.lane * 16;
@@ -301,17 +265,6 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
     }
   }
 #endif
-}
-
-// s_waitcnt vmcnt(k) for a k that is a constant only after unrolling.
-__device__ __forceinline__ void wait_vmcnt(int k) {
-#define NERF_VM(N) else if (k == N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");
-  if (k <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  NERF_VM(1) NERF_VM(2) NERF_VM(3) NERF_VM(4) NERF_VM(5) NERF_VM(6) NERF_VM(7) NERF_VM(8)
-  NERF_VM(10) NERF_VM(12) NERF_VM(14) NERF_VM(15) NERF_VM(16) NERF_VM(18) NERF_VM(20) NERF_VM(21)
-  NERF_VM(24) NERF_VM(28) NERF_VM(30) NERF_VM(32)
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#undef NERF_VM
 }
 
 // Chunks whose LDS-DMA may still be in flight after stage(g+2) has landed:
@@ -422,8 +375,8 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
 #pragma unroll
           for (int c = 0; c < kCols; ++c) {
             const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
-            const f32x4 b0 = ds_read_f4(cx.bias_addr, off), b1 = ds_read_f4(cx.bias_addr, off + 16);
-            const f32x4 b2 = ds_read_f4(cx.bias_addr, off + 32), b3 = ds_read_f4(cx.bias_addr, off + 48);
+            const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
+            const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
             acc[c][2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
                                         b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
           }

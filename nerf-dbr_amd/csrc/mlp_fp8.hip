@@ -1,0 +1,351 @@
+// fp8 (OCP e4m3) NeRF MLP on gfx950: v_mfma_scale_f32_32x32x64_f8f6f4, fp32
+// accumulate.  The compressed-weights path (BASELINE config 5): the reference's
+// counterpart is the int8 CompressedNeRFRenderer
+// (src/benchmark/compressed_renderer.py:89-211), whose error vs fp32 is the
+// baseline this path is reported against.
+//
+// Same network, orientation and schedule as mlp_bf16.hip (nerf_layout.h):
+// H^T = W . X^T on 32x32 tiles, the accumulator of one layer is the B operand
+// of the next, 8 waves x 32 samples, quarter schedule, an LDS ring filled by
+// LDS-DMA with one barrier per chunk, asm fragment reads with counted waits.
+// What differs:
+//   * k-steps are 64 wide: a hidden k-step takes accumulator tiles 2u, 2u+1;
+//     a 256-wide layer has 4 k-steps (vs 16 in bf16), each MFMA is 64 cycles
+//     and does 4x the work of a bf16 one, at twice the bf16 FLOP rate;
+//   * weights are e4m3 with a power-of-two (E8M0) scale per output row, chosen
+//     at packing so no row saturates; the MFMA applies it (scale_a operand);
+//   * activations are e4m3 with a per-sample power-of-two scale: a sample's
+//     largest ReLU output of the previous layer maps into [128, 256), so
+//     nothing can overflow to NaN (e4m3fn has no infinity); the MFMA applies
+//     the scale back (scale_b).  The running maximum is gathered during the
+//     previous layer's quarters, so only its last two tiles are reduced at the
+//     layer boundary;
+//   * encodings are e4m3 at scale 1 (|sin|,|cos| <= 1; positions clamped to
+//     +-448).
+// Bias, ReLU, the density and colour heads and everything outside the MLP stay
+// fp32.
+#include "nerf_asm.h"
+#include "nerf_device.h"
+#include "nerf_internal.h"
+
+namespace nerf {
+namespace {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;           // 256
+constexpr int kUnitB = kFp8UnitBytes;                                // 4 KiB: 2 tiles x 64 lanes x 32 B
+constexpr int kUnits = kFp8Units;                                    // 130
+constexpr int kChunkUnits = 4;
+constexpr int kChunkB = kChunkUnits * kUnitB;                        // 16 KiB
+constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
+constexpr int kSlots = 4;
+constexpr int kPf = 2;                                               // fragment prefetch distance (units)
+constexpr int kRing = kPf + 1;
+constexpr int kGldsPerStage = kChunkB / (kThreads * 16);
+static_assert(kTotalChunks * kChunkB <= kFp8ScaleOff, "ring reads stay inside the padded fragment area");
+static_assert(kSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
+constexpr int kLdsParamOff = kSlots * kChunkB;
+constexpr int kLdsScaleOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
+constexpr int kLdsPeOff = kLdsScaleOff + kFp8ScaleBytes;
+constexpr int kLdsDeOff = kLdsPeOff + kWaves * 2048;
+constexpr int kLdsBytes = kLdsDeOff + kWaves * 2048;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+static_assert(kFp8ScaleBytes % 16 == 0 && kLdsScaleOff % 16 == 0, "16-B aligned carve");
+
+// ---- compile-time unit map ----
+NL_HD int unit_layer(int n) {
+  int l = 0;
+  while (l + 1 < kNumMfmaLayers && fp8_unit_base(l + 1) <= n) ++l;
+  return l;
+}
+NL_HD int unit_kstep(int n) { return (n - fp8_unit_base(unit_layer(n))) % ksteps_fp8(unit_layer(n)); }
+NL_HD int unit_extra(int n) {
+  const int l = unit_layer(n);
+  return unit_kstep(n) < layer_shape(l).hidden / 64 ? 0 : layer_shape(l).extra;
+}
+NL_HD bool unit_opens_quarter(int n) { return unit_kstep(n) == 0; }
+NL_HD int unit_reads(int n) { return n < 0 || n >= kUnits ? 0 : 4 + (unit_extra(n) != 0 ? 2 : 0); }
+constexpr int kQuarterReads = 8 + 1;          // bias (2 tiles x 4 x 16 B) + the weight-scale pair
+NL_HD int quarter_reads(int m) { return m >= 0 && m < kUnits && unit_opens_quarter(m) ? kQuarterReads : 0; }
+// Issue order per unit body m: [bias + scale reads if m opens a quarter],
+// reads of unit m+kPf, wait, MFMAs.  LDS reads younger than all unit n needs:
+NL_HD int lgkm_for_unit(int n) {
+  if (unit_opens_quarter(n)) return unit_reads(n + kPf);
+  int c = 0;
+  for (int k = n + 1; k <= n + kPf; ++k) c += unit_reads(k);
+  for (int m = n - kPf + 1; m <= n; ++m) c += quarter_reads(m);
+  return c;
+}
+
+struct Ctx {
+  const char* blob;
+  char* lds;
+  int wave_u, lane, h;
+  unsigned ring_addr, pe_addr, de_addr, bias_addr, scale_addr;
+};
+
+__device__ __forceinline__ void stage_chunk(const Ctx& cx, int g) {
+  const char* src = cx.blob + size_t(g) * kChunkB + cx.wave_u * 1024 + cx.lane * 16;
+  char* dst = cx.lds + (g % kSlots) * kChunkB + cx.wave_u * 1024;
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i) lds_dma_16(src + i * kThreads * 16, lds_addr(dst + i * kThreads * 16));
+}
+
+NL_HD int dma_outstanding_at_seam(int g) {
+  const int issued_last = (g + kSlots - 2 < kTotalChunks - 1) ? g + kSlots - 2 : kTotalChunks - 1;
+  return issued_last > g + 1 ? issued_last - (g + 1) : 0;
+}
+// Seam before the prefetch reaches chunk g+1 (protocol of mlp_bf16.hip):
+// own pieces of g+1 landed, barrier, restage chunk g-1's slot with g+kSlots-1.
+__device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
+  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
+  const int g = (n + kPf) / kChunkUnits - 1;
+  wait_vmcnt(kGldsPerStage * dma_outstanding_at_seam(g));
+  compiler_fence();
+  __builtin_amdgcn_s_barrier();
+  compiler_fence();
+  if (g + kSlots - 1 < kTotalChunks) stage_chunk(cx, g + kSlots - 1);
+}
+
+__device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
+  return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Unit n -> ring entry n % kRing: two A fragments (32 B per lane each, as two
+// lane-linear 16-B halves) and, for an encoding k-step, the B fragment.
+__device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing]) {
+  const int off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
+#pragma unroll
+  for (int o2 = 0; o2 < 2; ++o2)
+    ra[n % kRing][o2] = join(ds_read_b128<i32x4>(cx.ring_addr, off + o2 * 2048),
+                             ds_read_b128<i32x4>(cx.ring_addr, off + o2 * 2048 + 1024));
+  const int ex = unit_extra(n);
+  if (ex != 0) {
+    const unsigned base = ex == kPos ? cx.pe_addr : cx.de_addr;
+    rb[n % kRing] = join(ds_read_b128<i32x4>(base, 0), ds_read_b128<i32x4>(base, 1024));
+  }
+}
+
+// fp32 <-> int32 bit patterns, by value: __builtin_bit_cast applied directly to
+// an ext_vector element lvalue (t[i]) reinterprets the vector's first element
+// instead (seen with this hipcc), so elements always pass through a scalar.
+__device__ __forceinline__ int f2i(float x) { return __builtin_bit_cast(int, x); }
+__device__ __forceinline__ float i2f(int x) { return __builtin_bit_cast(float, x); }
+
+// Four e4m3 bytes from four fp32 values x / s (RNE), low byte first.
+__device__ __forceinline__ int cvt4_scaled(float a, float b, float c, float d, float s) {
+  i16x2 w = {0, 0};
+  w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, a, b, s, false);
+  w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, c, d, s, true);
+  return __builtin_bit_cast(int, w);
+}
+__device__ __forceinline__ int cvt4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+
+// Tiles 2u, 2u+1 of the previous layer -> B fragment of hidden k-step u
+// (byte j: register j&15 of tile 2u + (j>>4)), ReLU'd and divided by the
+// sample's activation scale s.  Before C0 the ReLU'd fp32 values also feed the
+// density head (nerf.py:114).
+template <bool kDensity>
+__device__ __forceinline__ void convert_pair(const f32x16& t0, const f32x16& t1, i32x8& b, float s, float& dens,
+                                             const Ctx& cx, int u) {
+  // ReLU on the bit patterns (signed max with 0: negative floats are negative
+  // int32), one v_max_i32 per value and no NaN canonicalising
+  float v[32];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    v[i] = i2f(__builtin_elementwise_max(f2i(t0[i]), 0));
+    v[16 + i] = i2f(__builtin_elementwise_max(f2i(t1[i]), 0));
+  }
+#pragma unroll
+  for (int d = 0; d < 8; ++d) b[d] = cvt4_scaled(v[4 * d], v[4 * d + 1], v[4 * d + 2], v[4 * d + 3], s);
+  if (kDensity) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = 2 * u + k;
+      const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 w = w4[q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dens = fmaf(w[i], v[16 * k + 4 * q + i], dens);
+      }
+    }
+    asm volatile("" : "+v"(dens));
+  }
+}
+
+// Running max of ReLU outputs on the fp32 bit patterns: a negative float is a
+// negative int32 and non-negative floats order like their bits, so a signed
+// integer max started at 0 is max(relu(x)) -- v_max3_i32, no NaN canonicalising.
+__device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t1) {
+#pragma unroll
+  for (int i = 0; i < 16; i += 2)
+    m = __builtin_elementwise_max(m, __builtin_elementwise_max(f2i(t0[i]), f2i(t0[i + 1])));
+#pragma unroll
+  for (int i = 0; i < 16; i += 2)
+    m = __builtin_elementwise_max(m, __builtin_elementwise_max(f2i(t1[i]), f2i(t1[i + 1])));
+  return m;
+}
+
+template <int L>
+__device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x8 (&ra)[kRing][2],
+                                          i32x8 (&rb)[kRing], int& amax, float& dens, const Ctx& cx) {
+  constexpr LayerShape sh = layer_shape(L);
+  constexpr int KH = sh.hidden / 64;
+  constexpr int KU = ksteps_fp8(L);
+  constexpr int NQ = out_tiles(L) / 2;
+  constexpr int N0 = fp8_unit_base(L);
+  constexpr bool kConvert = L != L0;
+  constexpr bool kDensity = L == C0;
+  constexpr bool kNextConverts = L != C0;        // the following layer reads these accumulators
+  float s = 1.0f;
+  int sb = 127;                                  // E8M0 of the activation scale (1.0 for encodings)
+  if (kConvert) {
+    // per-sample scale: the largest ReLU output of the previous layer -> [128, 256)
+    int mb = max_pair(amax, acc[6], acc[7]);
+    mb = __builtin_elementwise_max(mb, __shfl_xor(mb, 32));
+    const int e = __builtin_amdgcn_frexp_expf(i2f(mb)) - 8;   // max = f * 2^(e+8), f in [0.5, 1)
+    s = __builtin_ldexpf(1.0f, e);
+    sb = 127 + e;
+    convert_pair<kDensity>(acc[0], acc[1], bh[0], s, dens, cx, 0);
+  }
+  amax = 0;
+  int sa0 = 127, sa1 = 127;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int n = N0 + q * KU + u;
+      seam_before(cx, n);
+      if (u == 0) {
+        // bias pre-load of the quarter's two tiles (straight into the accumulators)
+        // and the E8M0 weight scales of their rows
+#pragma unroll
+        for (int o2 = 0; o2 < 2; ++o2) {
+          const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
+          const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
+          const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
+          acc[2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                   b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+        }
+        const u32x2 sc = ds_read_b64(cx.scale_addr, (L * 4 + q) * 512);
+        sa0 = int(sc[0]);
+        sa1 = int(sc[1]);
+      }
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      wait_lgkm(lgkm_for_unit(n));
+      const bool hidden = u < KH;
+      const i32x8 b = hidden ? bh[hidden ? u : 0] : rb[n % kRing];
+      const int sbu = hidden ? sb : 127;
+      acc[2 * q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][0], b, acc[2 * q], 0, 0, 0, sa0, 0,
+                                                                  sbu);
+      acc[2 * q + 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][1], b, acc[2 * q + 1], 0, 0, 0,
+                                                                      sa1, 0, sbu);
+      // conversion slices: tiles (2u+2, 2u+3) -> k-step u+1, before quarter 0 reads it
+      if (kConvert && q == 0 && u < 3) convert_pair<kDensity>(acc[2 * u + 2], acc[2 * u + 3], bh[u + 1], s, dens, cx, u + 1);
+      // running maximum for the next layer's scale: the previous quarter's tiles are final
+      if (kNextConverts && q >= 1 && u == (KU > 1 ? 1 : 0)) amax = max_pair(amax, acc[2 * q - 2], acc[2 * q - 1]);
+    }
+  }
+}
+
+template <bool kExplicit>
+__global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __restrict__ blob,
+                                                              const float* __restrict__ prm_g, SampleSrc src,
+                                                              long n_points, f32x4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  const int lane = threadIdx.x & 63;
+  const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  const unsigned base = lds_addr(lds);
+  const Ctx cx{blob, lds, wave_u, lane, h,
+               base + lane * 16,
+               base + kLdsPeOff + wave_u * 2048 + lane * 16,
+               base + kLdsDeOff + wave_u * 2048 + lane * 16,
+               base + kLdsParamOff + h * 64,
+               base + kLdsScaleOff + lane * 8};
+  const long p = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
+
+#pragma unroll
+  for (int g = 0; g < kSlots - 1; ++g) stage_chunk(cx, g);
+  for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
+    ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
+  for (int i = threadIdx.x; i < kFp8ScaleBytes / 16; i += kThreads)
+    ((f32x4*)(lds + kLdsScaleOff))[i] = ((const f32x4*)(blob + kFp8ScaleOff))[i];
+  {
+    float x[3], d[3], pef[32], def[16];
+    fetch_sample<kExplicit>(src, p < n_points ? p : n_points - 1, x, d);
+    pos_encode<true>(x[0], x[1], x[2], h, pef);
+    dir_encode<true>(d[0], d[1], d[2], h, def);
+    // raw coordinates (slots 30, 31 of half 0, slot 30 of half 1) clamped to the e4m3 range
+    pef[30] = __builtin_fminf(__builtin_fmaxf(pef[30], -kFp8Max), kFp8Max);
+    pef[31] = __builtin_fminf(__builtin_fmaxf(pef[31], -kFp8Max), kFp8Max);
+    i32x4* pe_dst = (i32x4*)(lds + kLdsPeOff + wave_u * 2048 + lane * 16);
+    i32x4* de_dst = (i32x4*)(lds + kLdsDeOff + wave_u * 2048 + lane * 16);
+    i32x4 w0, w1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w0[i] = cvt4(pef[4 * i], pef[4 * i + 1], pef[4 * i + 2], pef[4 * i + 3]);
+      w1[i] = cvt4(pef[16 + 4 * i], pef[16 + 4 * i + 1], pef[16 + 4 * i + 2], pef[16 + 4 * i + 3]);
+    }
+    pe_dst[0] = w0;
+    pe_dst[64] = w1;                                   // +1024 B: the second 16-B half
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w0[i] = cvt4(def[4 * i], def[4 * i + 1], def[4 * i + 2], def[4 * i + 3]);
+    de_dst[0] = w0;
+    de_dst[64] = i32x4{0, 0, 0, 0};                    // direction slots 16..31: padding
+  }
+  wait_vmcnt(kGldsPerStage * (kSlots - 2));            // chunk 0 landed (own pieces)
+  __syncthreads();
+  i32x8 ra[kRing][2], rb[kRing];
+#pragma unroll
+  for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+
+  f32x16 acc[8];
+  i32x8 bh[4];
+  int amax = 0;
+  float dens = 0.0f;
+  layer_fp8<L0>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L1>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L2>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L3>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L4>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L5>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L6>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<L7>(acc, bh, ra, rb, amax, dens, cx);
+  layer_fp8<C0>(acc, bh, ra, rb, amax, dens, cx);
+  const float* prm = (const float*)(lds + kLdsParamOff);
+  const float sigma = relu(dens + __shfl_xor(dens, 32) + prm[kSigB]);
+  relu_tiles<4>(acc);
+  float rgb[3];
+  color_head(acc, prm, h, rgb);
+  if (p < n_points && h == 0) out[p] = f32x4{sigma, rgb[0], rgb[1], rgb[2]};
+}
+
+}  // namespace
+
+hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
+                          bool explicit_points, hipStream_t stream) {
+  if (n_points <= 0) return hipSuccess;
+  const long blocks = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
+  const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
+  if (explicit_points)
+    hipLaunchKernelGGL(mlp_fp8_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
+                       (f32x4*)out);
+  else
+    hipLaunchKernelGGL(mlp_fp8_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
+                       (f32x4*)out);
+  return hipGetLastError();
+}
+
+}  // namespace nerf

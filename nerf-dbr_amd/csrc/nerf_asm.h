@@ -1,0 +1,82 @@
+// Inline-asm building blocks shared by the MFMA kernels' weight streams.
+//
+// Why asm: when hipcc sees an LDS-DMA (global_load_lds) in a function it stops
+// counting LDS waits and emits lgkmcnt(0) before every fragment use, and left to
+// itself it puts one s_waitcnt in front of nearly every MFMA.  The kernels
+// instead issue the DMA and every in-loop LDS read from asm and wait with
+// compile-time counts.  An asm destination counts as written at the statement,
+// so every counted wait is followed by a sched_barrier that keeps the
+// consumers behind it (cdna_hip_programming.md §5.7 rule 18).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace nerf {
+
+typedef float asm_f32x4 __attribute__((ext_vector_type(4)));
+typedef int asm_i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned asm_u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// LDS byte address of a __shared__ object (for asm operands)
+template <typename T>
+__device__ __forceinline__ unsigned lds_addr(T* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)p;
+}
+
+// 16-B LDS read; off must fold to a constant in [0, 65536) after unrolling
+template <typename V>
+__device__ __forceinline__ V ds_read_b128(unsigned addr, int off) {
+  static_assert(sizeof(V) == 16, "16-byte fragment");
+  V v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  return v;
+}
+__device__ __forceinline__ asm_u32x2 ds_read_b64(unsigned addr, int off) {
+  asm_u32x2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
+  return v;
+}
+
+// s_waitcnt lgkmcnt(k), k a constant after unrolling, then a scheduling barrier
+// so nothing that consumes the reads moves above it.  The field is 4 bits on
+// gfx9: k > 15 waits at 15, i.e. for more reads than needed (safe).
+__device__ __forceinline__ void wait_lgkm(int k) {
+#define NERF_LG(N) else if (k == N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory");
+  if (k <= 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  NERF_LG(1) NERF_LG(2) NERF_LG(3) NERF_LG(4) NERF_LG(5) NERF_LG(6) NERF_LG(7) NERF_LG(8) NERF_LG(9)
+  NERF_LG(10) NERF_LG(11) NERF_LG(12) NERF_LG(13) NERF_LG(14)
+  else asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+#undef NERF_LG
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// s_waitcnt vmcnt(k) for a k that is a constant only after unrolling.
+__device__ __forceinline__ void wait_vmcnt(int k) {
+#define NERF_VM(N) else if (k == N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");
+  if (k <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  NERF_VM(1) NERF_VM(2) NERF_VM(3) NERF_VM(4) NERF_VM(5) NERF_VM(6) NERF_VM(7) NERF_VM(8)
+  NERF_VM(10) NERF_VM(12) NERF_VM(14) NERF_VM(15) NERF_VM(16) NERF_VM(18) NERF_VM(20) NERF_VM(21)
+  NERF_VM(24) NERF_VM(28) NERF_VM(30) NERF_VM(32)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef NERF_VM
+}
+
+// One lane-linear 1 KiB LDS-DMA piece per wave: 16 B per lane from src to
+// LDS byte address lds_base + lane*16 (wave-uniform base in M0, saved and
+// restored inside the statement).  Completion is tracked with vmcnt.
+__device__ __forceinline__ void lds_dma_16(const void* src, unsigned lds_base) {
+  unsigned keep;
+  const unsigned base = __builtin_amdgcn_readfirstlane(lds_base);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(base)
+      : "memory");
+}
+
+}  // namespace nerf

@@ -17,6 +17,8 @@ hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSr
                           float* out, bool explicit_points, hipStream_t stream);
 hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points,
                            float* out, bool explicit_points, hipStream_t stream);
+hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points,
+                          float* out, bool explicit_points, hipStream_t stream);
 hipError_t launch_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride,
                             const float* z, int z_ray_stride, const float* rays_d, int n_rays, int n_samples,
                             float* rgb_out, float* depth_out, float* acc_out, float* weights_out,

@@ -144,4 +144,42 @@ NL_HD int bf16_blob_chunks() {
 // so any kernel chunk geometry of up to 32 units reads inside the buffer.
 constexpr int kBf16BlobBytes = ((bf16_unit_base(kNumMfmaLayers) + 31) / 32) * 32 * kUnitBytes;
 
+// ------------------------------------------------------------------ fp8 --
+// v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 A and B (OCP e4m3fn).  Lane half h
+// supplies 32 bytes of a k-step of 64; byte j of A (row r) and byte j of B
+// (column c) carry the same k (pinned on hardware, tools/probes).  A hidden
+// k-step u takes accumulator tiles 2u and 2u+1 of the previous layer: byte j
+// of lane half h is register j&15 of tile 2u + (j>>4), i.e. row
+// 32(2u + (j>>4)) + acc_row(j&15, h).  An encoding k-step takes the 32 slots
+// of pe_slot_feature / dpe_slot_feature (direction: slots 16..31 padding).
+// Scales are E8M0 bytes: weights per output row (fixed at packing), the
+// previous layer's activations per sample (computed in the kernel).
+NL_HD int hid_fp8_feature(int u, int h, int j) { return 32 * (2 * u + (j >> 4)) + acc_row(j & 15, h); }
+NL_HD int ksteps_fp8(int l) { LayerShape s = layer_shape(l); return s.hidden / 64 + (s.extra != kNone ? 1 : 0); }
+NL_HD int fp8_k_col(int l, int u, int h, int j) {
+  LayerShape s = layer_shape(l);
+  int nh = s.hidden / 64;
+  if (u < nh) return hid_fp8_feature(u, h, j);
+  int f = s.extra == kPos ? pe_slot_feature(h, j) : (j < 16 ? dpe_slot_feature(h, j) : -1);
+  return f < 0 ? -1 : s.hidden + f;
+}
+// fp8 A blob: 4 KiB units (layer, quarter q, k-step u) = [tile-in-quarter o2][lane 64][32 B],
+// in the bf16 blob's quarter order, zero-padded to a multiple of 8 units (each
+// lane's 32 B split into two 16 B halves p: [o2][p][lane][16 B], so every
+// ds_read_b128 is lane-linear); then the weight scales: per layer [quarter 4]
+// [lane 64][o2 2] u32 whose low byte is the E8M0 scale of row 32*(2q+o2) + (lane&31).
+constexpr int kFp8UnitBytes = 4096;
+NL_HD int fp8_layer_units(int l) { return (out_tiles(l) / 2) * ksteps_fp8(l); }
+NL_HD int fp8_unit_base(int l) {
+  int n = 0;
+  for (int i = 0; i < l; ++i) n += fp8_layer_units(i);
+  return n;
+}
+constexpr int kFp8Units = fp8_unit_base(kNumMfmaLayers);                        // 130
+constexpr int kFp8UnitsPadded = ((kFp8Units + 7) / 8) * 8;                      // 136
+constexpr int kFp8ScaleOff = kFp8UnitsPadded * kFp8UnitBytes;                   // bytes
+constexpr int kFp8ScaleBytes = kNumMfmaLayers * 4 * 64 * 2 * 4;
+constexpr int kFp8BlobBytes = kFp8ScaleOff + kFp8ScaleBytes;
+constexpr float kFp8Max = 448.0f;                                              // largest finite e4m3fn
+
 }  // namespace nerf

@@ -27,7 +27,83 @@ uint16_t f32_to_bf16_rne(float f) {
   return uint16_t(u >> 16);
 }
 
+// f32 -> OCP e4m3fn, round to nearest even; |v| <= 448 is the caller's contract
+// (the packer picks power-of-two scales that guarantee it).  Subnormals: 2^-9 steps.
+uint8_t f32_to_e4m3_rne(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  const uint8_t sign = uint8_t((u >> 24) & 0x80u);
+  float a = std::fabs(v);
+  if (!(a == a)) return 0x7F;                          // NaN
+  if (a == 0.0f) return sign;
+  int e;
+  std::frexp(a, &e);                                   // a = m * 2^e, m in [0.5, 1)
+  int ex = e - 1;                                      // a in [2^ex, 2^(ex+1))
+  if (ex < -6) ex = -6;                                // subnormal range shares 2^-9 steps
+  const float step = std::ldexp(1.0f, ex - 3);         // 3 mantissa bits
+  float q = std::nearbyint(a / step) * step;           // default rounding mode: nearest even
+  if (q == 0.0f) return sign;
+  std::frexp(q, &e);
+  ex = e - 1;
+  if (ex < -6) return uint8_t(sign | uint8_t(q / std::ldexp(1.0f, -9)));           // subnormal: mantissa only
+  const int mant = int(q / std::ldexp(1.0f, ex - 3)) - 8;                          // 0..7
+  return uint8_t(sign | uint8_t((ex + 7) << 3) | uint8_t(mant));
+}
+
+// E8M0 exponent e (value 2^e) so that max|row| / 2^e <= 448
+int row_scale_exp(float max_abs) {
+  if (!(max_abs > 0.0f)) return 0;
+  int e = int(std::ceil(std::log2(double(max_abs) / double(kFp8Max))));
+  while (std::ldexp(double(max_abs), -e) > kFp8Max) ++e;
+  while (std::ldexp(double(max_abs), -(e - 1)) <= kFp8Max) --e;
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
 }  // namespace
+
+extern "C" size_t nerf_fp8_blob_bytes(void) { return size_t(kFp8BlobBytes); }
+
+extern "C" void nerf_f32_to_e4m3(const float* x, int n, uint8_t* out) {
+  for (int i = 0; i < n; ++i) out[i] = f32_to_e4m3_rne(x[i]);
+}
+
+extern "C" int nerf_pack_weights_fp8(const float* const* params, int n_params, uint8_t* blob) {
+  if (!params || n_params != NERF_N_PARAMS || !blob)
+    return set_error(NERF_E_INVALID, "nerf_pack_weights_fp8: need %d tensors and a blob", NERF_N_PARAMS);
+  for (int i = 0; i < NERF_N_PARAMS; ++i)
+    if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_fp8: tensor %d is NULL", i);
+  auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * kSpecIn[spec] + k]; };
+  std::memset(blob, 0, size_t(kFp8BlobBytes));
+  uint8_t* dst = blob;
+  uint32_t* scales = reinterpret_cast<uint32_t*>(blob + kFp8ScaleOff);
+  for (int l = 0; l < kNumMfmaLayers; ++l) {
+    const int spec = kSpecOfLayer[l], nt = out_tiles(l), ku = ksteps_fp8(l), nq = nt / 2;
+    int exps[256];
+    for (int row = 0; row < 32 * nt; ++row) {
+      float m = 0.0f;
+      for (int k = 0; k < kSpecIn[spec]; ++k) m = std::fmax(m, std::fabs(W(spec, row, k)));
+      exps[row] = row_scale_exp(m);
+    }
+    for (int q = 0; q < 4; ++q)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int o2 = 0; o2 < 2; ++o2) {
+          const int tile = 2 * q + o2;
+          scales[((l * 4 + q) * 64 + lane) * 2 + o2] = tile < nt ? uint32_t(127 + exps[32 * tile + (lane & 31)]) : 127u;
+        }
+    for (int q = 0; q < nq; ++q)
+      for (int u = 0; u < ku; ++u)
+        for (int o2 = 0; o2 < 2; ++o2)
+          for (int p = 0; p < 2; ++p)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int jj = 0; jj < 16; ++jj) {
+                const int j = 16 * p + jj;
+                const int col = fp8_k_col(l, u, lane >> 5, j);
+                const int row = 32 * (2 * q + o2) + (lane & 31);
+                *dst++ = col < 0 ? uint8_t(0) : f32_to_e4m3_rne(std::ldexp(W(spec, row, col), -exps[row]));
+              }
+  }
+  return NERF_OK;
+}
 
 extern "C" void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob) {
   if (f32_blob) *f32_blob = size_t(f32_blob_floats()) * sizeof(float);

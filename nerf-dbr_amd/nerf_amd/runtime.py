@@ -24,13 +24,13 @@ LIB_NAME = "libnerf_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", LIB_NAME)
 
 NERF_OK = 0
-NERF_FP32, NERF_BF16 = 0, 1
+NERF_FP32, NERF_BF16, NERF_FP8 = 0, 1, 2
 NERF_NET_COARSE, NERF_NET_FINE = 0, 1
 NERF_N_PARAMS = 22
 NERF_N_STAGES = 5
 STAGES = ("rays", "coarse_mlp", "importance", "fine_mlp", "composite")
 
-PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16}
+PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16, "fp8": NERF_FP8}
 
 # Every symbol include/nerf_mi355x.h declares, with its ctypes signature.
 _c = ctypes
@@ -46,6 +46,9 @@ SIGNATURES = {
     "nerf_packed_sizes": (None, [_c.POINTER(_c.c_size_t)] * 3),
     "nerf_pack_weights": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P, _P, _P]),
     "nerf_uniform_z": (None, [_FP, _c.c_int, _c.c_float, _c.c_float, _FP]),
+    "nerf_fp8_blob_bytes": (_c.c_size_t, []),
+    "nerf_pack_weights_fp8": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P]),
+    "nerf_f32_to_e4m3": (None, [_FP, _c.c_int, _P]),
     "nerf_generate_rays": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _P, _P, _P]),
     "nerf_mlp_forward": (_c.c_int, [_P, _c.c_int, _c.c_int, _P, _P, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P]),
     "nerf_query": (_c.c_int, [_P, _c.c_int, _c.c_int, _P, _P, _c.c_int, _P, _P]),
@@ -124,6 +127,25 @@ def pack_weights(sd: Mapping[str, np.ndarray]):
                                  prm.ctypes.data_as(_P)))
     del keep
     return f32, bf, prm
+
+
+def pack_weights_fp8(sd: Mapping[str, np.ndarray]) -> np.ndarray:
+    """Host-only fp8 packing (e4m3 fragments + E8M0 row scales), as the loader runs it."""
+    lib = load_library()
+    blob = np.zeros(lib.nerf_fp8_blob_bytes(), np.uint8)
+    keep, ptrs = _param_list(sd)
+    _check(lib.nerf_pack_weights_fp8(ptrs, NERF_N_PARAMS, blob.ctypes.data_as(_P)))
+    del keep
+    return blob
+
+
+def f32_to_e4m3(x: np.ndarray) -> np.ndarray:
+    """The library's f32 -> e4m3fn rounding (uint8 codes)."""
+    lib = load_library()
+    a = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.zeros(a.size, np.uint8)
+    lib.nerf_f32_to_e4m3(_fptr(a), a.size, out.ctypes.data_as(_P))
+    return out.reshape(np.shape(x))
 
 
 def uniform_z(t_vals: np.ndarray, near: float, far: float) -> np.ndarray:

@@ -239,3 +239,77 @@ def test_fp32_emulation_matches_reference_golden(samples):
     s_emu, rgb_emu = emulate(f32, bf, prm, pe, dpe, "fp32")
     np.testing.assert_allclose(s_emu, g["sigma_fine"][idx, 0], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(rgb_emu.T, g["rgb_fine"][idx], rtol=0, atol=1e-6)
+
+
+# ------------------------------------------------------------------ fp8 path --
+def e4m3_round(x):
+    """torch's f32 -> float8_e4m3fn (RNE) and back."""
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.float8_e4m3fn).float().numpy().astype(np.float64)
+
+
+def e4m3_decode(codes):
+    return torch.from_numpy(np.ascontiguousarray(codes, np.uint8)).view(torch.float8_e4m3fn).float().numpy()
+
+
+def test_f32_to_e4m3_matches_torch():
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.standard_normal(20000) * s for s in (1e-3, 0.05, 1, 30, 150)]).astype(np.float32)
+    x = np.concatenate([x, [0.0, -0.0, 448.0, -448.0, 2.0 ** -9, 2.0 ** -10, 3 * 2.0 ** -10, 2.0 ** -6, 1.0625,
+                            1.1875, 240.0, 232.0, 447.9]]).astype(np.float32)
+    x = np.clip(x, -448, 448)
+    ours = rt.f32_to_e4m3(x)
+    ref = torch.from_numpy(x).to(torch.float8_e4m3fn).view(torch.uint8).numpy()
+    assert np.array_equal(ours, ref)
+
+
+def emulate_fp8(blob, prm, pe, dpe):
+    """Kernel lane maps of the fp8 path (nerf_layout.h), float64 accumulation."""
+    n = pe.shape[1]
+    scale_off = 136 * 4096
+    scales = blob[scale_off:].view(np.uint32).reshape(9, 4, 64, 2)
+    off = 0
+    x = x7 = None
+    for li, (_, out, hidden, extra) in enumerate(LAYERS):
+        nt, nq = out // 32, out // 64
+        ku = hidden // 64 + (1 if extra else 0)
+        acc = np.tile(unpack_bias(prm, li, nt)[:, None], (1, n))
+        raw = blob[off: off + nq * ku * 4096]
+        off += nq * ku * 4096
+        a = e4m3_decode(raw).reshape(nq, ku, 2, 2, 64, 16)            # [q][u][o2][p][lane][16]
+        a = a.transpose(0, 1, 2, 4, 3, 5).reshape(nq, ku, 2, 64, 32)   # [q][u][o2][lane][byte j]
+        if x is not None:
+            e = O.fp8_activation_exponent(x)
+            xq = e4m3_round(np.maximum(x, 0) / np.ldexp(1.0, e)) * np.ldexp(1.0, e)
+        if extra:
+            feats, fn, used = (pe, pe_slot_feature, 32) if extra == "pos" else (dpe, dpe_slot_feature, 16)
+            ext = [e4m3_round(np.stack([feats[fn(h, j)] if (j < used and fn(h, j) >= 0) else np.zeros(n)
+                                        for j in range(32)])) for h in range(2)]
+        for q in range(nq):
+            for o2 in range(2):
+                t = 2 * q + o2
+                for lane in range(64):
+                    r, h = lane & 31, lane >> 5
+                    s = np.ldexp(1.0, int(scales[li, q, lane, o2] & 0xFF) - 127)
+                    row = 32 * t + r
+                    for u in range(ku):
+                        if u < hidden // 64:
+                            b = xq[[32 * (2 * u + (j >> 4)) + acc_row(j & 15, h) for j in range(32)]]
+                        else:
+                            b = ext[h]
+                        acc[row] += s * (a[q, u, o2, lane].astype(np.float64) @ b)
+        x = np.maximum(acc, 0)
+        if li == 7:
+            x7 = x
+    return heads(prm, x7, x)
+
+
+def test_fp8_packing_computes_the_mlp(samples):
+    pe, dpe, _, _ = samples
+    sd = W.synthetic_state_dict(1)
+    blob = rt.pack_weights_fp8(sd)
+    _, _, prm = rt.pack_weights(sd)
+    assert blob.size == 136 * 4096 + 9 * 4 * 64 * 2 * 4
+    s_emu, rgb_emu = emulate_fp8(blob, prm, pe[:, :6], dpe[:, :6])
+    s_dir, rgb_dir = O.fp8_mlp_restated(sd, pe[:, :6], dpe[:, :6])
+    np.testing.assert_allclose(s_emu, s_dir, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(rgb_emu, rgb_dir, rtol=1e-6, atol=1e-6)

@@ -59,7 +59,7 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
-    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--precision", choices=sorted(rt.PRECISIONS), default="bf16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--spp", type=int, default=128)
     args = ap.parse_args()
