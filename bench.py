@@ -42,7 +42,62 @@ def parse():
     ap.add_argument("--spp", type=int, default=128)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0: skip)")
     ap.add_argument("--no-error-check", action="store_true", help="skip the bf16-vs-fp32 error band")
+    ap.add_argument("--no-extras", action="store_true", help="skip the other BASELINE configs (C2, C3, C5)")
     return ap.parse_args()
+
+
+def time_frames(render, n_warm, n_steps):
+    """Mean seconds per call of render() (device-synchronised)."""
+    import torch
+
+    for _ in range(n_warm):
+        render()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_steps):
+        render()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n_steps
+
+
+def other_configs(ckpt, pose, local, ref32):
+    """The BASELINE configs besides the headline, 1 GPU each:
+    C2 400x300x64 fp32 (the parity path), C3 800x600 64+128 hierarchical bf16,
+    C5 800x600x128 fp8."""
+    from nerf_amd import weights as W
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    out = {}
+    dt = time_frames(lambda: ref32.render_rows(pose, (400, 300), 64, 0, 300), 1, 3)
+    out["c2_fp32_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt}
+
+    h = MI355XRenderer("bf16", n_importance=128, device_index=local)
+    h.setup(ckpt)
+    h.hip.set_profiling(True)
+    dt = time_frames(lambda: h.render_rows(pose, (800, 600), 64, 0, 600), 2, 5)
+    st = h.hip.stage_ms()
+    flop = 800 * 600 * (64 + 192) * W.FLOPS_PER_SAMPLE
+    mlp_ms = st["coarse_mlp"] + st["fine_mlp"]
+    out["c3_hierarchical_bf16_800x600_64+128"] = {
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms": st,
+        "mlp_tflops": flop / (mlp_ms * 1e-3) / 1e12, "mlp_frac_bf16_peak": flop / (mlp_ms * 1e-3) / 1e12 / 2500.0,
+        "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)"}
+
+    f8 = MI355XRenderer("fp8", device_index=local)
+    f8.setup(ckpt)
+    f8.hip.set_profiling(True)
+    dt = time_frames(lambda: f8.render_rows(pose, (800, 600), 128, 0, 600), 2, 5)
+    ms = f8.hip.stage_ms()["fine_mlp"]
+    tf = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE / (ms * 1e-3) / 1e12
+    rgb8, d8 = f8.render_rows(pose, (800, 600), 128, 292, 308)
+    rgb32, d32 = ref32.render_rows(pose, (800, 600), 128, 292, 308)
+    out["c5_fp8_800x600x128"] = {
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms, "mlp_tflops": tf,
+        "mlp_frac_fp8_peak": tf / PEAK_TFLOPS["fp8"],
+        "rgb_max_abs_vs_fp32": float((rgb8 - rgb32).abs().max()),
+        "rgb_mean_abs_vs_fp32": float((rgb8 - rgb32).abs().mean()),
+        "depth_max_abs_vs_fp32": float((d8 - d32).abs().max())}
+    return out
 
 
 def cpu_baseline(pose, width, height, spp, target_s):
@@ -69,6 +124,9 @@ def cpu_baseline(pose, width, height, spp, target_s):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line; the renderers' reference-style
+    # progress messages go to stderr
+    json_out, sys.stdout = sys.stdout, sys.stderr
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -143,10 +201,12 @@ def main():
     peak = PEAK_TFLOPS[args.precision]
 
     extra = {}
-    if rank == 0 and args.precision != "fp32" and not args.no_error_check:
-        # bf16 / fp8 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
+    ref = None
+    if rank == 0 and ((args.precision != "fp32" and not args.no_error_check) or (world == 1 and not args.no_extras)):
         ref = MI355XRenderer("fp32", device_index=local)
         ref.setup(ckpt)
+    if rank == 0 and args.precision != "fp32" and not args.no_error_check:
+        # bf16 / fp8 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
         a0, a1 = height // 2 - 8, height // 2 + 8
         rgb32, d32 = ref.render_rows(pose, (width, height), spp, a0, a1)
         rgb_lp, d_lp = r.render_rows(pose, (width, height), spp, a0, a1)
@@ -158,6 +218,9 @@ def main():
         ref.render_rows(pose, (width, height), spp, 0, height)
         torch.cuda.synchronize()
         extra["fp32_path_rays_per_s_1gpu"] = width * height / (time.perf_counter() - t1)
+
+    if rank == 0 and world == 1 and not args.no_extras:
+        extra["other_configs"] = other_configs(ckpt, pose, local, ref)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -187,7 +250,7 @@ def main():
             "cpu_baseline": cpu,
         }
         out.update(extra)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
