@@ -295,3 +295,88 @@ def fp8_mlp_restated(sd, pe, dpe):
     rgb = 1 / (1 + np.exp(-(sd["color_layers.1.weight"].astype(np.float64) @ hcol
                             + sd["color_layers.1.bias"][:, None])))
     return sigma, rgb
+
+
+# ------------------------------------- reference compressed renderer (int8) --
+# Restatement of CompressedNeRFRenderer (src/benchmark/compressed_renderer.py) in
+# its default configuration, as the error baseline of the fp8 path (SURVEY §8f
+# row 2).  Pinned by tests/golden/compressed.npz (make_golden_compressed.py).
+COMPRESSED_CONFIG = {"quantization_bits": 8, "pruning_ratio": 0.1, "use_mixed_precision": True,
+                     "compress_activations": True}                       # compressed_renderer.py:27-32
+
+
+def compressed_weights(sd: Mapping[str, np.ndarray], bits: int = 8, pruning: float = 0.1) -> Dict[str, torch.Tensor]:
+    """Per tensor (weights and biases alike): magnitude pruning at the `pruning`
+    quantile (compressed_renderer.py:89-104), then asymmetric int8 quantisation
+    with scale (max-min)/255 and a rounded zero point (:106-145), dequantised back
+    to fp32 for compute (:147-159)."""
+    out = {}
+    qmin, qmax = -(2 ** (bits - 1)), 2 ** (bits - 1) - 1
+    for name, arr in sd.items():
+        w = torch.from_numpy(np.ascontiguousarray(arr, np.float32)).clone()
+        if pruning > 0:
+            thr = torch.quantile(w.flatten().abs(), pruning)
+            w = w * (w.abs() > thr).float()
+        w_min, w_max = w.min().item(), w.max().item()
+        if w_max == w_min:
+            out[name] = w                       # :117-118 (scale 1, zero point 0: unchanged)
+            continue
+        scale = (w_max - w_min) / (qmax - qmin)
+        zp = torch.round(torch.clamp(torch.tensor(qmin - w_min / scale), qmin, qmax)).int()
+        q = torch.clamp(torch.round(w / scale + zp), qmin, qmax).to(torch.int8)
+        out[name] = (q.float() - zp.item()) * scale
+    return out
+
+
+def _compressed_pe(x: torch.Tensor, n_freqs: int) -> torch.Tensor:
+    enc = [x]                                   # compressed_renderer.py:58-65
+    for i in range(n_freqs):
+        freq = 2.0 ** i
+        enc.append(torch.sin(freq * torch.pi * x))
+        enc.append(torch.cos(freq * torch.pi * x))
+    return torch.cat(enc, dim=-1)
+
+
+def compressed_query(cw: Mapping[str, torch.Tensor], positions, directions):
+    """_compressed_mlp_forward (compressed_renderer.py:161-211): fp16 linear layers."""
+    def lin(x, name):
+        return F.linear(x.half(), cw[f"{name}.weight"].half(), cw[f"{name}.bias"].half()).float()
+
+    pe, de = _compressed_pe(_t(positions), 10), _compressed_pe(_t(directions), 4)
+    with torch.no_grad():
+        x = pe
+        for i in range(8):
+            if i == 4:
+                x = torch.cat([x, pe], dim=1)
+            x = torch.relu(lin(x, f"layers.{i}"))
+        density = torch.relu(lin(x, "density_head"))
+        h = torch.relu(lin(torch.cat([x, de], dim=1), "color_layers.0"))
+        color = torch.sigmoid(lin(h, "color_layers.1"))
+    return density, color
+
+
+def compressed_composite(sigma, rgb, z, rays_d):
+    """execute_volume_rendering of the compressed renderer (:233-269): last interval
+    1e4 and fp16 alpha compositing."""
+    dists = z[..., 1:] - z[..., :-1]
+    dists = torch.cat([dists, torch.full_like(dists[..., :1], 1e4)], dim=-1)
+    dists = dists * torch.norm(rays_d[..., None, :], dim=-1)
+    sigma, rgb, dists = sigma.half(), rgb.half(), dists.half()
+    alpha = 1.0 - torch.exp(-F.relu(sigma[..., 0]) * dists)
+    trans = torch.cumprod(1.0 - alpha + 1e-10, dim=-1)
+    trans = torch.cat([torch.ones_like(trans[..., :1]), trans[..., :-1]], dim=-1)
+    w = alpha * trans
+    return torch.sum(w[..., None] * rgb, dim=-2).float(), torch.sum(w * z, dim=-1).float()
+
+
+def compressed_render_image(cw: Mapping[str, torch.Tensor], c2w, resolution: Tuple[int, int], n_samples: int = 64):
+    """CompressedNeRFRenderer.render_image (:311-355): all rays in one query, no chunking."""
+    width, height = resolution
+    rays_o, rays_d = generate_rays(c2w, width, height)
+    o, d = rays_o.reshape(-1, 3), rays_d.reshape(-1, 3)
+    z = uniform_z(n_samples).expand(o.shape[0], n_samples)
+    pts = sample_points(o, d, z)
+    dirs = d[:, None, :].expand(-1, n_samples, -1).reshape(-1, 3)
+    s, c = compressed_query(cw, pts.reshape(-1, 3), dirs)
+    rgb, depth = compressed_composite(s.reshape(-1, n_samples, 1), c.reshape(-1, n_samples, 3), z, d)
+    return rgb.reshape(height, width, 3), depth.reshape(height, width)

@@ -1,0 +1,61 @@
+"""Golden vectors of the reference's int8 CompressedNeRFRenderer.
+
+Run in the development container only (the reference is not on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_compressed.py [/root/reference]
+
+Imports src/benchmark/compressed_renderer.py (default config: 10 % magnitude
+pruning and int8 asymmetric per-tensor quantisation of every weight and bias,
+fp16 linear layers, fp16 compositing with a 1e4 last interval), sets it up on
+the same deterministic synthetic checkpoint as make_golden.py, and records:
+  compressed.npz  query_nerf_networks (fine) on the first 512 points of mlp.npz,
+                  and render_image at 32x24, 16 samples, suite view 0.
+These pin the oracle's restatement (oracle/nerf_oracle.py, compressed_*), which
+is the error baseline the fp8 path is reported against; the reference's
+compressed renderer is not a parity target.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "nerf-dbr_amd"))
+
+from nerf_amd import weights as W  # noqa: E402
+
+
+def main(ref_root: str = "/root/reference") -> None:
+    import torch
+
+    sys.path.insert(0, ref_root)
+    import src  # noqa: F401
+
+    bp = types.ModuleType("src.benchmark")
+    bp.__path__ = [os.path.join(ref_root, "src", "benchmark")]
+    sys.modules["src.benchmark"] = bp
+    from src.benchmark.compressed_renderer import CompressedNeRFRenderer
+
+    ckpt = W.write_synthetic_checkpoint(os.path.join(tempfile.mkdtemp(), "synthetic.pth"), seed=0)
+    r = CompressedNeRFRenderer()
+    r.setup(ckpt)
+    g = np.load(os.path.join(HERE, "mlp.npz"))
+    pos, dirs = torch.from_numpy(g["pos"][:512]), torch.from_numpy(g["dirs"][:512])
+    with torch.no_grad():
+        sigma, rgb = r.query_nerf_networks(pos, dirs, use_fine=True)
+        pose = torch.eye(4)
+        pose[2, 3] = 4.0
+        img, depth = r.render_image(pose, (32, 24), 16)
+    np.savez_compressed(os.path.join(HERE, "compressed.npz"), pos=g["pos"][:512], dirs=g["dirs"][:512],
+                        sigma=sigma.float().numpy(), rgb=rgb.float().numpy(), pose=pose.numpy(),
+                        image=img.float().numpy(), depth=depth.float().numpy())
+    print("compressed.npz:", sigma.shape, rgb.shape, img.shape, float(img.min()), float(img.max()))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")

@@ -352,3 +352,24 @@ def test_render_fp8_error_vs_fp32(r8, r32, golden):
     print(f"fp8 vs fp32 800x600x128 band: rgb max {er:.3e} mean {mr:.3e}, depth max {ed:.3e}")
     assert torch.isfinite(rgb8).all() and torch.isfinite(d8).all()
     assert er < 0.1 and mr < 0.01
+
+
+def test_fp8_error_below_reference_compressed(r8, r32):
+    """Config 5's error baseline: the reference's own compressed (int8, pruned,
+    fp16) renderer, restated in the oracle and pinned to its golden vectors.  The
+    fp8 path must be closer to fp32 than the reference's compressed path is."""
+    from oracle import nerf_oracle as O
+
+    _, f = W.synthetic_models(0)
+    pose = torch.eye(4)
+    pose[2, 3] = 4.0
+    w, h, s = 64, 48, 32
+    rgb32, d32 = r32.render_image(pose, (w, h), s)
+    rgb8, d8 = r8.render_image(pose, (w, h), s)
+    rgbc, dc = O.compressed_render_image(O.compressed_weights(f), pose, (w, h), s)
+    e8, ec = maxabs(rgb8, rgb32.cpu().numpy()), maxabs(rgbc, rgb32.cpu().numpy())
+    m8 = float((rgb8 - rgb32).abs().mean())
+    mc = float((rgbc - rgb32.cpu()).abs().mean())
+    print(f"vs fp32 at {w}x{h}x{s}: fp8 rgb max {e8:.3e} mean {m8:.3e}; "
+          f"reference int8 compressed rgb max {ec:.3e} mean {mc:.3e}")
+    assert e8 < ec and m8 < mc

@@ -130,3 +130,14 @@ def test_importance_sample_properties():
     # every coarse sample survives the merge
     for r in range(0, n, 16):
         assert set(z[r].tolist()) <= set(zf[r].tolist())
+
+
+def test_compressed_restatement_matches_reference(golden):
+    """The reference's int8 compressed renderer (fp8 path's error baseline)."""
+    g = golden("compressed")
+    _, f = W.synthetic_models(0)
+    cw = O.compressed_weights(f)
+    s, c = O.compressed_query(cw, torch.from_numpy(g["pos"]), torch.from_numpy(g["dirs"]))
+    assert np.array_equal(s.numpy(), g["sigma"]) and np.array_equal(c.numpy(), g["rgb"])
+    rgb, depth = O.compressed_render_image(cw, torch.from_numpy(g["pose"]), (32, 24), 16)
+    assert np.array_equal(rgb.numpy(), g["image"]) and np.array_equal(depth.numpy(), g["depth"])
