@@ -134,6 +134,149 @@ __global__ void importance_kernel(const float* __restrict__ z_coarse, int z_ray_
   while (ic < n_coarse) out[o++] = zr[ic++];
 }
 
+// The same sampler, one wave per ray, bit-identical to importance_kernel:
+//  * the normaliser and the cdf are the same sequential double sums -- every lane
+//    runs the same ordered loop over the ray's weights (LDS broadcast reads) and
+//    keeps the cdf entries of its own indices, so no per-thread array (scratch);
+//  * searchsorted(cdf, u, right=True) is a binary search for the count of cdf
+//    entries <= u, which equals the linear scan on a nondecreasing cdf;
+//  * the merge writes every sample at its rank: importance sample k lands at
+//    k + #{coarse z <= z_k}, coarse sample i at i + #{importance z < z_i} --
+//    the sequential merge's order whenever both lists are nondecreasing (true for
+//    sorted z and ascending u); otherwise lane 0 merges sequentially.
+constexpr int kMaxImpWave = 1024;
+constexpr int kImpWaves = 4;
+
+__device__ __forceinline__ int count_le(const float* a, int n, float v) {   // #{i < n : a[i] <= v}
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int count_lt(const float* a, int n, float v) {   // #{i < n : a[i] < v}
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(64 * kImpWaves) void importance_wave_kernel(
+    const float* __restrict__ z_coarse, int z_ray_stride, const float* __restrict__ weights,
+    const float* __restrict__ u, int u_ray_stride, int n_rays, int n_coarse, int n_importance,
+    float* __restrict__ z_fine) {
+  __shared__ float s_a[kImpWaves][kMaxCoarse];
+  __shared__ float s_cdf[kImpWaves][kMaxCoarse + 1];
+  __shared__ float s_z[kImpWaves][kMaxCoarse];
+  __shared__ float s_zs[kImpWaves][kMaxImpWave];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long r = long(blockIdx.x) * kImpWaves + wv;
+  if (r >= n_rays) return;                                     // wave-uniform
+  const float* zr = z_coarse + r * z_ray_stride;
+  const float* wr = weights + r * n_coarse;
+  const float* ur = u + r * u_ray_stride;
+  float* out = z_fine + r * (n_coarse + n_importance);
+  float* a = s_a[wv];
+  float* cdf = s_cdf[wv];
+  float* zc = s_z[wv];
+  float* zs = s_zs[wv];
+  for (int i = lane; i < n_coarse; i += 64) {
+    a[i] = __fadd_rn(wr[i], 1e-5f);
+    zc[i] = zr[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double sum = 0.0;
+  for (int i = 0; i < n_coarse; ++i) sum = __dadd_rn(sum, double(a[i]));
+  const float total = float(sum);
+  sum = 0.0;
+  if (lane == 0) cdf[0] = 0.0f;
+  for (int i = 0; i < n_coarse; ++i) {
+    sum = __dadd_rn(sum, double(__fdiv_rn(a[i], total)));
+    if ((i & 63) == lane) cdf[i + 1] = float(sum);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  bool mono = true;
+  for (int k = lane; k < n_importance; k += 64) {
+    const float uk = ur[k];
+    const int idx = count_le(cdf, n_coarse + 1, uk);
+    const int below = min(max(idx - 1, 0), n_coarse - 1);
+    const int above = min(max(idx, 0), n_coarse - 1);
+    const float cb = cdf[below], ca = cdf[above];
+    float denom = __fsub_rn(ca, cb);
+    if (denom < 1e-5f) denom = 1.0f;
+    const float t = __fdiv_rn(__fsub_rn(uk, cb), denom);
+    const float zb = zc[below];
+    zs[k] = __fadd_rn(zb, __fmul_rn(t, __fsub_rn(zc[above], zb)));
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int k = lane + 1; k < n_importance; k += 64) mono = mono && !(zs[k] < zs[k - 1]);
+  for (int i = lane + 1; i < n_coarse; i += 64) mono = mono && !(zc[i] < zc[i - 1]);
+  if (__all(mono)) {
+    for (int k = lane; k < n_importance; k += 64) out[k + count_le(zc, n_coarse, zs[k])] = zs[k];
+    for (int i = lane; i < n_coarse; i += 64) out[i + count_lt(zs, n_importance, zc[i])] = zc[i];
+  } else if (lane == 0) {
+    int ic = 0, o = 0;
+    for (int k = 0; k < n_importance; ++k) {
+      while (ic < n_coarse && zc[ic] <= zs[k]) out[o++] = zc[ic++];
+      out[o++] = zs[k];
+    }
+    while (ic < n_coarse) out[o++] = zc[ic++];
+  }
+}
+
+// Compositing of the render path's packed MLP output (sigma, r, g, b) per
+// sample: the arithmetic of composite_kernel, with 16-B loads issued eight
+// samples at a time (whole cache lines per request).
+__global__ void composite_packed_kernel(const f32x4* __restrict__ mlp, const float* __restrict__ z, int z_ray_stride,
+                                        const float* __restrict__ rays_d, int n_rays, int n_samples,
+                                        float* __restrict__ rgb_out, float* __restrict__ depth_out,
+                                        float* __restrict__ acc_out, float* __restrict__ weights_out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float dx = rays_d[3L * r], dy = rays_d[3L * r + 1], dz = rays_d[3L * r + 2];
+  const float norm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+  const float* zr = z + long(r) * z_ray_stride;
+  const long base = long(r) * n_samples;
+  double T_acc = 1.0;
+  float cr = 0.0f, cg = 0.0f, cb = 0.0f, dep = 0.0f, acc = 0.0f;
+  for (int s0 = 0; s0 < n_samples; s0 += 8) {
+    f32x4 v[8];
+    float zz[9];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = s0 + j < n_samples ? mlp[base + s0 + j] : f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 9; ++j) zz[j] = s0 + j < n_samples ? zr[s0 + j] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int s = s0 + j;
+      if (s >= n_samples) break;
+      const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(zz[j + 1], zz[j]) : 1e10f, norm);
+      const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-relu(v[j][0]), dist)));
+      const float w = __fmul_rn(alpha, float(T_acc));
+      cr = __fadd_rn(cr, __fmul_rn(w, v[j][1]));
+      cg = __fadd_rn(cg, __fmul_rn(w, v[j][2]));
+      cb = __fadd_rn(cb, __fmul_rn(w, v[j][3]));
+      dep = __fadd_rn(dep, __fmul_rn(w, zz[j]));
+      acc = __fadd_rn(acc, w);
+      if (weights_out) weights_out[base + s] = w;
+      T_acc = __dmul_rn(T_acc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
+    }
+  }
+  rgb_out[3L * r] = cr;
+  rgb_out[3L * r + 1] = cg;
+  rgb_out[3L * r + 2] = cb;
+  depth_out[r] = dep;
+  if (acc_out) acc_out[r] = acc;
+}
+
 // Sample depths and points, one thread per (ray, sample).
 // Uniform (BaseUnifiedRenderer.sample_points_on_rays, base_renderer.py:260-281):
 //   z = table[s] (near*(1-t)+far*t, built on the host bit-exactly).
@@ -198,6 +341,12 @@ hipError_t launch_composite(const float* sigma, int sigma_stride, const float* r
   if (n_rays <= 0) return hipSuccess;
   const int threads = 128;
   const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  if (sigma_stride == 4 && rgb_stride == 4 && rgb == sigma + 1 && n_samples > 1 &&
+      (reinterpret_cast<uintptr_t>(sigma) & 15) == 0) {
+    hipLaunchKernelGGL(composite_packed_kernel, grid, block, 0, stream, (const f32x4*)sigma, z, z_ray_stride, rays_d,
+                       n_rays, n_samples, rgb_out, depth_out, acc_out, weights_out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(composite_kernel, grid, block, 0, stream, sigma, sigma_stride, rgb, rgb_stride, z, z_ray_stride,
                      rays_d, n_rays, n_samples, rgb_out, depth_out, acc_out, weights_out);
   return hipGetLastError();
@@ -208,6 +357,12 @@ hipError_t launch_importance(const float* z_coarse, int z_ray_stride, const floa
                              hipStream_t stream) {
   if (n_rays <= 0) return hipSuccess;
   if (n_coarse > kMaxCoarse) return hipErrorInvalidValue;
+  if (n_importance <= kMaxImpWave) {
+    const dim3 grid{unsigned((n_rays + kImpWaves - 1) / kImpWaves), 1, 1}, block{64 * kImpWaves, 1, 1};
+    hipLaunchKernelGGL(importance_wave_kernel, grid, block, 0, stream, z_coarse, z_ray_stride, weights, u,
+                       u_ray_stride, n_rays, n_coarse, n_importance, z_fine);
+    return hipGetLastError();
+  }
   const int threads = 64;
   const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
   hipLaunchKernelGGL(importance_kernel, grid, block, 0, stream, z_coarse, z_ray_stride, weights, u, u_ray_stride,
