@@ -119,7 +119,13 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
 #else
     // issued from inline asm (nerf_asm.h): the builtin makes hipcc emit lgkmcnt(0)
     // before every fragment use; completion is tracked by counted vmcnt + barrier
+#ifdef NERF_BF16_VADDR_GLDS
     lds_dma_16(src + i * kThreads * 16, lds_addr(dst + i * kThreads * 16));
+#else
+    (void)src;
+    lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
+                 lds_addr(dst + i * kThreads * 16));
+#endif
 #endif
   }
 }
@@ -162,6 +168,8 @@ __device__ __forceinline__ bf16x8 pack8_relu(const f32x16& a, int base) {
 constexpr int kStampBlocks = 256;
 constexpr unsigned kStampFirst = 8192;   // steady state: well past the cold-L2 first wave of blocks
 __device__ unsigned long long g_nerf_stamps[kStampBlocks][kWaves][kStampSlots];
+// shader clock vs the 100 MHz constant clock over each wave's life (clock = dt/drt * 100 MHz)
+__device__ unsigned long long g_nerf_clock[kStampBlocks][kWaves][4];
 #define NERF_STAMP(cx, i)                                                                             \
   do {                                                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                                \
@@ -202,6 +210,23 @@ __device__ __forceinline__ void convert_tile(const f32x16& acc_t, bf16x8& b0, bf
     }
     // pin the partial sum here: sinking these FMAs to the kernel's end would keep
     // the layer's accumulators alive through C0 (and spill them)
+    asm volatile("" : "+v"(dens));
+  }
+}
+
+// Half a tile (registers 8s..8s+7 = k-step 2t+s of the next layer), for the
+// spread schedule below.
+template <bool kDensity>
+__device__ __forceinline__ void convert_half(const f32x16& acc_t, int s, bf16x8& b, float& dens, const Ctx& cx, int t) {
+  b = pack8_relu(acc_t, 8 * s);
+  if (kDensity) {
+    const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
+#pragma unroll
+    for (int q = 2 * s; q < 2 * s + 2; ++q) {
+      const f32x4 w = w4[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dens = fmaf(w[i], relu(acc_t[4 * q + i]), dens);
+    }
     asm volatile("" : "+v"(dens));
   }
 }
@@ -325,8 +350,18 @@ __device__ __forceinline__ void after_unit(const Ctx& cx, int n) {
 }
 #endif
 
+// Conversion schedule (default): layer L's output tiles 2q-2, 2q-1 become final
+// at the end of its quarter q-1 and are converted to the next layer's B
+// fragments (bout) in four half-tile slices during quarter q = 1..3; tiles 6, 7
+// follow in the next layer's quarter 0 (into its bin, before k-step 12 reads
+// them).  Two tiles per quarter, nothing exposed at the layer boundary, and each
+// fp32 tile dies as soon as it is packed.  -DNERF_BF16_LATE_CVT restores the
+// earlier schedule (all eight tiles converted around the next layer's quarter 0).
+// Slice j (0..3) of a quarter runs at unit kSlicePos(KU, j).
+NL_HD int slice_pos(int ku, int j) { return ku >= 12 ? 2 + 3 * j : j; }
+
 template <int L>
-__device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)[kCols][16],
+__device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)[kCols][16], bf16x8 (&bout)[kCols][16],
                                            bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], float (&dens)[kCols],
                                            const Ctx& cx) {
   constexpr LayerShape sh = layer_shape(L);
@@ -337,6 +372,14 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
   constexpr bool kConvert = L != L0;          // B fragments come from the previous layer
   constexpr bool kDensity = L == C0;          // ... which, before C0, also feeds the density head
   [[maybe_unused]] const float* prm = (const float*)(cx.lds + kLdsParamOff);
+#ifndef NERF_BF16_LATE_CVT
+  constexpr bool kConvertOut = L != C0;       // this layer's outputs feed another MFMA layer
+  constexpr bool kDensityOut = L == L7;
+  (void)bout;
+#else
+  (void)bout;
+#endif
+#ifdef NERF_BF16_LATE_CVT
   if (kConvert) {
     // This wave's reads of the previous layer's last units are issued; the
     // conversion of tiles 0-1 is the only part not hidden behind MFMAs.
@@ -345,6 +388,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
 #pragma unroll
       for (int c = 0; c < kCols; ++c) convert_tile<kDensity>(acc[c][t], bh[c][2 * t], bh[c][2 * t + 1], dens[c], cx, t);
   }
+#endif
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
 #ifdef NERF_BF16_CC_LDS
@@ -400,6 +444,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
         for (int c = 0; c < kCols; ++c)
           acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][o2], b[c], acc[c][2 * q + o2],
                                                                       0, 0, 0);
+#ifdef NERF_BF16_LATE_CVT
       // conversion slices: the (tile, column) pairs of tiles 2..7 spread over
       // k-steps 0..11, one tile per two k-steps (tile t done before k-step 2t)
       if (kConvert && q == 0 && u < 12 && (u % (2 / kCols)) == 0) {
@@ -407,6 +452,22 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
         const int t = 2 + i / kCols, c = i % kCols;
         convert_tile<kDensity>(acc[c][t], bh[c][2 * t], bh[c][2 * t + 1], dens[c], cx, t);
       }
+#else
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (u != slice_pos(KU, j)) continue;
+        const int t = j >> 1, half = j & 1;
+        if (kConvert && q == 0)       // previous layer's tiles 6, 7 -> this layer's k-steps 12..15
+#pragma unroll
+          for (int c = 0; c < kCols; ++c)
+            convert_half<kDensity>(acc[c][6 + t], half, bh[c][2 * (6 + t) + half], dens[c], cx, 6 + t);
+        if (kConvertOut && q >= 1)    // this layer's tiles 2q-2, 2q-1 -> the next layer's k-steps
+#pragma unroll
+          for (int c = 0; c < kCols; ++c)
+            convert_half<kDensityOut>(acc[c][2 * q - 2 + t], half, bout[c][2 * (2 * q - 2 + t) + half], dens[c], cx,
+                                      2 * q - 2 + t);
+      }
+#endif
       after_unit(cx, n);
     }
   }
@@ -427,6 +488,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
                lds_base + kLdsParamOff + h * 64};
   const long p0 = (long(blockIdx.x) * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
   NERF_STAMP(cx, 0);
+#ifdef NERF_STAMPS
+  const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // Kick off the weight stream, then do the per-sample prologue under it.
 #ifndef NERF_BF16_SEAM_OLD
@@ -480,19 +544,33 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 #endif
 
   f32x16 acc[kCols][8];
-  bf16x8 bh[kCols][16];
   float dens[kCols];
 #pragma unroll
   for (int c = 0; c < kCols; ++c) dens[c] = 0.0f;
-  layer_bf16<L0>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<L1>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<L2>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<L3>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<L4>(acc, bh, ra, rb, dens, cx);   // skip: [x, pe] (nerf.py:109-110)
-  layer_bf16<L5>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<L6>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<L7>(acc, bh, ra, rb, dens, cx);
-  layer_bf16<C0>(acc, bh, ra, rb, dens, cx);   // [x, PE4(d)] (nerf.py:117-121); density head folded in
+#ifndef NERF_BF16_LATE_CVT
+  // two B-fragment sets: layer l reads one while it fills the other for l+1
+  bf16x8 bA[kCols][16], bB[kCols][16];
+  layer_bf16<L0>(acc, bB, bA, ra, rb, dens, cx);
+  layer_bf16<L1>(acc, bA, bB, ra, rb, dens, cx);
+  layer_bf16<L2>(acc, bB, bA, ra, rb, dens, cx);
+  layer_bf16<L3>(acc, bA, bB, ra, rb, dens, cx);
+  layer_bf16<L4>(acc, bB, bA, ra, rb, dens, cx);   // skip: [x, pe] (nerf.py:109-110)
+  layer_bf16<L5>(acc, bA, bB, ra, rb, dens, cx);
+  layer_bf16<L6>(acc, bB, bA, ra, rb, dens, cx);
+  layer_bf16<L7>(acc, bA, bB, ra, rb, dens, cx);
+  layer_bf16<C0>(acc, bB, bA, ra, rb, dens, cx);   // [x, PE4(d)] (nerf.py:117-121); density head folded in
+#else
+  bf16x8 bh[kCols][16];
+  layer_bf16<L0>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L1>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L2>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L3>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L4>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L5>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L6>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<L7>(acc, bh, bh, ra, rb, dens, cx);
+  layer_bf16<C0>(acc, bh, bh, ra, rb, dens, cx);
+#endif
   const float* prm = (const float*)(lds + kLdsParamOff);
 #pragma unroll
   for (int c = 0; c < kCols; ++c) {
@@ -505,6 +583,13 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   }
 #ifdef NERF_STAMPS
   NERF_STAMP(cx, kStampSlots - 1);
+  if (blockIdx.x - kStampFirst < kStampBlocks && lane == 0) {
+    unsigned long long* c = g_nerf_clock[blockIdx.x - kStampFirst][wave_u];
+    c[0] = clk_t0;
+    c[1] = clk_r0;
+    c[2] = __builtin_amdgcn_s_memtime();
+    c[3] = __builtin_amdgcn_s_memrealtime();
+  }
   if (blockIdx.x - kStampFirst < kStampBlocks && lane == 0)
     for (int i = 0; i < kStampSlots; ++i)
       g_nerf_stamps[blockIdx.x - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
@@ -538,5 +623,10 @@ extern "C" int nerf_debug_stamps(void* host, size_t bytes, int* waves, int* slot
   const size_t need = sizeof(nerf::g_nerf_stamps);
   if (bytes < need) return -1;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(nerf::g_nerf_stamps), need) == hipSuccess ? 0 : -2;
+}
+extern "C" int nerf_debug_clock(void* host, size_t bytes) {
+  const size_t need = sizeof(nerf::g_nerf_clock);
+  if (bytes < need) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nerf::g_nerf_clock), need) == hipSuccess ? 0 : -2;
 }
 #endif

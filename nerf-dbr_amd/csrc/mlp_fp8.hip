@@ -91,10 +91,11 @@ struct Ctx {
 };
 
 __device__ __forceinline__ void stage_chunk(const Ctx& cx, int g) {
-  const char* src = cx.blob + size_t(g) * kChunkB + cx.wave_u * 1024 + cx.lane * 16;
   char* dst = cx.lds + (g % kSlots) * kChunkB + cx.wave_u * 1024;
 #pragma unroll
-  for (int i = 0; i < kGldsPerStage; ++i) lds_dma_16(src + i * kThreads * 16, lds_addr(dst + i * kThreads * 16));
+  for (int i = 0; i < kGldsPerStage; ++i)
+    lds_dma_16_s(cx.blob + size_t(g) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
+                 lds_addr(dst + i * kThreads * 16));
 }
 
 NL_HD int dma_outstanding_at_seam(int g) {

@@ -85,7 +85,14 @@ def main():
         skew["inter_simd_spread_med"] = float(np.median(pair_last.max(axis=1) - pair_last.min(axis=1)))
         # which wave of a pair is late, as a fraction of seams
         skew["upper_wave_late_frac"] = float((arrive[:, 4:] > arrive[:, :4]).mean())
+    clk = np.zeros(256 * waves.value * 4, np.uint64)
+    fc = lib.lib.nerf_debug_clock
+    fc.restype, fc.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]
+    assert fc(clk.ctypes.data, clk.nbytes) == 0
+    clk = clk.reshape(256, waves.value, 4).astype(np.float64)
+    ghz = (clk[..., 2] - clk[..., 0]) / np.maximum(clk[..., 3] - clk[..., 1], 1) * 0.1
     out = {
+        "in_kernel_clock_ghz_median": float(np.median(ghz)),
         "kernel_ms": ms, "waves": waves.value, "chunks": n_chunks, "skew": skew,
         "total_med": float(np.median(total)), "prologue_med": float(np.median(prologue)),
         "compute_med": float(np.median(compute.sum(2))), "wait_med": float(np.median(waits.sum(2))),
