@@ -46,18 +46,47 @@ __device__ __forceinline__ void pe_sincos(float c, float x, float* s, float* co)
 
 // Position encoding slots of lane half h (nerf_layout.h pe_slot_feature):
 // 15 sin/cos pairs + the raw coordinates it owns.
+// Fast path: a lane half's frequencies are consecutive powers of two, so after
+// one reduced sin/cos per coordinate the rest follow by angle doubling,
+// sin 2t = 2 s c, cos 2t = 1 - 2 s^2.  The doubled argument 2^j * fl(2^k pi x)
+// equals the reference's fl(2^(k+j) pi x) exactly (power-of-two scaling); the
+// doubling adds ~1e-5 absolute error after four steps, far below bf16/e4m3
+// rounding of the encodings.
+template <int kFreqs>
+__device__ __forceinline__ void sincos_doubling(float c0, float x, float* s, float* co) {
+  sincos_fast(__fmul_rn(c0, x), &s[0], &co[0]);
+#pragma unroll
+  for (int k = 1; k < kFreqs; ++k) {
+    s[k] = 2.0f * (s[k - 1] * co[k - 1]);
+    co[k] = fmaf(-2.0f * s[k - 1], s[k - 1], 1.0f);
+  }
+}
+
 template <bool kFast = false>
 __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, float (&pe)[32]) {
-#pragma unroll
-  for (int kk = 0; kk < 5; ++kk) {
-    const float c = pe_coef(5 * h + kk);
-    const float xs[3] = {x0, x1, x2};
+  const float xs[3] = {x0, x1, x2};
+  if (kFast) {
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      float s, co;
-      pe_sincos<kFast>(c, xs[m], &s, &co);
-      pe[6 * kk + m] = s;
-      pe[6 * kk + 3 + m] = co;
+      float s[5], co[5];
+      sincos_doubling<5>(pe_coef(5 * h), xs[m], s, co);
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        pe[6 * kk + m] = s[kk];
+        pe[6 * kk + 3 + m] = co[kk];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const float c = pe_coef(5 * h + kk);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        float s, co;
+        pe_sincos<false>(c, xs[m], &s, &co);
+        pe[6 * kk + m] = s;
+        pe[6 * kk + 3 + m] = co;
+      }
     }
   }
   pe[30] = h ? x2 : x0;
@@ -66,16 +95,29 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
 
 template <bool kFast = false>
 __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, float (&de)[16]) {
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const float c = pe_coef(2 * h + kk);
-    const float ds[3] = {d0, d1, d2};
+  const float ds[3] = {d0, d1, d2};
+  if (kFast) {
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      float s, co;
-      pe_sincos<kFast>(c, ds[m], &s, &co);
-      de[6 * kk + m] = s;
-      de[6 * kk + 3 + m] = co;
+      float s[2], co[2];
+      sincos_doubling<2>(pe_coef(2 * h), ds[m], s, co);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        de[6 * kk + m] = s[kk];
+        de[6 * kk + 3 + m] = co[kk];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const float c = pe_coef(2 * h + kk);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        float s, co;
+        pe_sincos<false>(c, ds[m], &s, &co);
+        de[6 * kk + m] = s;
+        de[6 * kk + 3 + m] = co;
+      }
     }
   }
   de[12] = h ? d2 : d0;
@@ -84,7 +126,13 @@ __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, 
   de[15] = 0.0f;
 }
 
-__device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
+// ReLU on the bit pattern: a negative float is a negative int32 and max(bits, 0)
+// is +0 for it, x otherwise -- one v_max_i32 (a float max needs a NaN
+// canonicalisation first: two instructions).  A NaN stays a NaN when its sign
+// bit is clear, as torch.relu propagates it.
+__device__ __forceinline__ float relu(float x) {
+  return __builtin_bit_cast(float, __builtin_elementwise_max(__builtin_bit_cast(int, x), 0));
+}
 
 // torch.sigmoid: 1 / (1 + exp(-x))
 __device__ __forceinline__ float sigmoid_ref(float x) { return __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-x))); }
