@@ -373,3 +373,29 @@ def test_fp8_error_below_reference_compressed(r8, r32):
     print(f"vs fp32 at {w}x{h}x{s}: fp8 rgb max {e8:.3e} mean {m8:.3e}; "
           f"reference int8 compressed rgb max {ec:.3e} mean {mc:.3e}")
     assert e8 < ec and m8 < mc
+
+
+def test_plain_c_host_matches_python(r32, tmp_path):
+    """examples/render_c.c drives the C ABI with no Python in the process; its frame
+    equals the Python plugin's bit for bit (same weights, t table and stream order)."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(GOLDEN), "..", "examples", "render_c")
+    assert os.path.exists(exe), "build with `make -C examples` (done by __graft_entry__.build())"
+    _, f = W.synthetic_models(0)
+    with open(tmp_path / "params.bin", "wb") as fh:
+        for name, _, _ in W.LAYER_SPECS:
+            for suffix in ("weight", "bias"):
+                fh.write(np.ascontiguousarray(f[f"{name}.{suffix}"], np.float32).tobytes())
+    w, h, s = 64, 48, 32
+    t = torch.linspace(0, 1, s).numpy()
+    t.tofile(tmp_path / "t.bin")
+    res = subprocess.run([exe, str(tmp_path / "params.bin"), str(w), str(h), str(s), "0", str(tmp_path / "out.bin"),
+                          str(tmp_path / "t.bin")], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    out = np.fromfile(tmp_path / "out.bin", np.float32)
+    pose = torch.eye(4)
+    pose[2, 3] = 4.0
+    rgb, depth = r32.render_image(pose, (w, h), s)
+    assert np.array_equal(out[: w * h * 3], rgb.cpu().numpy().ravel())
+    assert np.array_equal(out[w * h * 3:], depth.cpu().numpy().ravel())
