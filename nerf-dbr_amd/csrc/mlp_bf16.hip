@@ -16,11 +16,11 @@
 // wave, accumulators in AGPRs.)
 //
 // Quarter schedule.  Each layer is issued in quarters of two output tiles.
-// The previous layer's accumulators are converted to bf16 fragments (ReLU'd),
-// and that conversion is VALU work the MFMA pipe would otherwise wait on.  Only
-// tiles 0-1 are converted up front; tiles 2-7 are converted in 12 slices
-// interleaved with quarter 0's MFMAs (their registers are first overwritten in
-// quarter 1, and k-step 2t first reads tile t's fragments after its slice).
+// A layer's output tiles are converted to the next layer's bf16 fragments
+// (ReLU'd) while the layer is still running: tiles 2q-2, 2q-1 during quarter
+// q, tiles 6-7 in the next layer's quarter 0, one dword (two values) per unit,
+// so the conversion is about one VALU per MFMA to issue under the other MFMAs
+// (see layer_bf16).
 //
 // Weight stream.  The packed blob is a sequence of 2 KiB units (layer, quarter,
 // k-step) cut into 16 KiB chunks.  A 4-slot LDS ring is filled by
@@ -192,33 +192,11 @@ struct Ctx {
   unsigned ring_addr, pe_addr, de_addr, bias_addr;
 };
 
-// Tile t of column c of the previous layer -> B fragments 2t, 2t+1 (register
-// 8s..8s+7 of tile t is k-step 2t+s; nerf_layout.h hid_bf16_feature).  Before
-// colour layer 0 the tile also feeds the density head (fp32, nerf.py:114).
-template <bool kDensity>
-__device__ __forceinline__ void convert_tile(const f32x16& acc_t, bf16x8& b0, bf16x8& b1, float& dens,
-                                             const Ctx& cx, int t) {
-  b0 = pack8_relu(acc_t, 0);
-  b1 = pack8_relu(acc_t, 8);
-  if (kDensity) {
-    const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = w4[q];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dens = fmaf(w[i], relu(acc_t[4 * q + i]), dens);
-    }
-    // pin the partial sum here: sinking these FMAs to the kernel's end would keep
-    // the layer's accumulators alive through C0 (and spill them)
-    asm volatile("" : "+v"(dens));
-  }
-}
-
 // Half a tile (registers 8s..8s+7 = k-step 2t+s of the next layer), for the
 // spread schedule below.
 template <bool kDensity>
-__device__ __forceinline__ void convert_half(const f32x16& acc_t, int s, bf16x8& b, float& dens, const Ctx& cx, int t) {
-  b = pack8_relu(acc_t, 8 * s);
+__device__ __forceinline__ void convert_half(const f32x16& acc_t, int s, u32x4& b, float& dens, const Ctx& cx, int t) {
+  b = __builtin_bit_cast(u32x4, pack8_relu(acc_t, 8 * s));
   if (kDensity) {
     const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
 #pragma unroll
@@ -355,13 +333,39 @@ __device__ __forceinline__ void after_unit(const Ctx& cx, int n) {
 // fragments (bout) in four half-tile slices during quarter q = 1..3; tiles 6, 7
 // follow in the next layer's quarter 0 (into its bin, before k-step 12 reads
 // them).  Two tiles per quarter, nothing exposed at the layer boundary, and each
-// fp32 tile dies as soon as it is packed.  -DNERF_BF16_LATE_CVT restores the
-// earlier schedule (all eight tiles converted around the next layer's quarter 0).
+// fp32 tile dies as soon as it is packed.
 // Slice j (0..3) of a quarter runs at unit kSlicePos(KU, j).
 NL_HD int slice_pos(int ku, int j) { return ku >= 12 ? 2 + 3 * j : j; }
+// Finer still for the layers without a density head: one dword (two values,
+// one v_cvt_pk_bf16_f32 + one v_pk_max_i16) per unit, so each wave has about
+// one conversion instruction per MFMA to issue under the other MFMAs instead
+// of a 16-instruction burst.  Dword m (0..15) of a tile pair: tile m>>3,
+// register pair m&7 -> fragment (m&7)>>2, dword m&3.
+NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }   // quarters 1..3
+NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }                                     // quarter 0, < 12
+__device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4& frag) {
+  frag[pr & 3] = cvt_relu_pair(tile[2 * pr], tile[2 * pr + 1]);
+}
+
+#ifndef NERF_BF16_CC_LDS
+// Bias pre-load of quarter q of layer l (tiles 2q, 2q+1), straight into the
+// accumulators (param blob [layer][tile][half][16]); l, q constant after unrolling.
+__device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (&acc)[kCols][8]) {
+#pragma unroll
+  for (int o2 = 0; o2 < 2; ++o2)
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      const int off = 4 * (kBiasOff + 256 * l + (2 * q + o2) * 32);
+      const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
+      const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
+      acc[c][2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                  b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+    }
+}
+#endif
 
 template <int L>
-__device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)[kCols][16], bf16x8 (&bout)[kCols][16],
+__device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[kCols][16], u32x4 (&bout)[kCols][16],
                                            bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], float (&dens)[kCols],
                                            const Ctx& cx) {
   constexpr LayerShape sh = layer_shape(L);
@@ -372,23 +376,8 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
   constexpr bool kConvert = L != L0;          // B fragments come from the previous layer
   constexpr bool kDensity = L == C0;          // ... which, before C0, also feeds the density head
   [[maybe_unused]] const float* prm = (const float*)(cx.lds + kLdsParamOff);
-#ifndef NERF_BF16_LATE_CVT
   constexpr bool kConvertOut = L != C0;       // this layer's outputs feed another MFMA layer
   constexpr bool kDensityOut = L == L7;
-  (void)bout;
-#else
-  (void)bout;
-#endif
-#ifdef NERF_BF16_LATE_CVT
-  if (kConvert) {
-    // This wave's reads of the previous layer's last units are issued; the
-    // conversion of tiles 0-1 is the only part not hidden behind MFMAs.
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int c = 0; c < kCols; ++c) convert_tile<kDensity>(acc[c][t], bh[c][2 * t], bh[c][2 * t + 1], dens[c], cx, t);
-  }
-#endif
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
 #ifdef NERF_BF16_CC_LDS
@@ -411,20 +400,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
       const int n = N0 + q * KU + u;
       seam_before(cx, n);
 #ifndef NERF_BF16_CC_LDS
-      if (u == 0) {
-        // bias pre-load of this quarter's two output tiles, straight into the
-        // accumulators (param blob: [layer][tile][half][16] floats)
-#pragma unroll
-        for (int o2 = 0; o2 < 2; ++o2)
-#pragma unroll
-          for (int c = 0; c < kCols; ++c) {
-            const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
-            const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
-            const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
-            acc[c][2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                                        b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
-          }
-      }
+      if (u == 0) issue_bias(cx, L, q, acc);   // this quarter's bias (waited with its first unit)
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
       wait_lgkm(lgkm_for_unit(n));
 #else
@@ -437,37 +413,44 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], bf16x8 (&bh)
 #endif
       bf16x8 b[kCols];
 #pragma unroll
-      for (int c = 0; c < kCols; ++c) b[c] = u < KH ? bh[c][u < KH ? u : 0] : rb[n % kRing][c];
+      for (int c = 0; c < kCols; ++c)
+        b[c] = u < KH ? __builtin_bit_cast(bf16x8, bh[c][u < KH ? u : 0]) : rb[n % kRing][c];
 #pragma unroll
       for (int o2 = 0; o2 < 2; ++o2)
 #pragma unroll
         for (int c = 0; c < kCols; ++c)
           acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][o2], b[c], acc[c][2 * q + o2],
                                                                       0, 0, 0);
-#ifdef NERF_BF16_LATE_CVT
-      // conversion slices: the (tile, column) pairs of tiles 2..7 spread over
-      // k-steps 0..11, one tile per two k-steps (tile t done before k-step 2t)
-      if (kConvert && q == 0 && u < 12 && (u % (2 / kCols)) == 0) {
-        const int i = u / (2 / kCols);
-        const int t = 2 + i / kCols, c = i % kCols;
-        convert_tile<kDensity>(acc[c][t], bh[c][2 * t], bh[c][2 * t + 1], dens[c], cx, t);
-      }
+#ifndef NERF_BF16_HALF_SLICES
+      constexpr bool kFineIn = !kDensity, kFineOut = !kDensityOut;
 #else
+      constexpr bool kFineIn = false, kFineOut = false;
+#endif
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (u != slice_pos(KU, j)) continue;
         const int t = j >> 1, half = j & 1;
-        if (kConvert && q == 0)       // previous layer's tiles 6, 7 -> this layer's k-steps 12..15
+        if (kConvert && !kFineIn && q == 0)       // previous layer's tiles 6, 7 -> this layer's k-steps 12..15
 #pragma unroll
           for (int c = 0; c < kCols; ++c)
             convert_half<kDensity>(acc[c][6 + t], half, bh[c][2 * (6 + t) + half], dens[c], cx, 6 + t);
-        if (kConvertOut && q >= 1)    // this layer's tiles 2q-2, 2q-1 -> the next layer's k-steps
+        if (kConvertOut && !kFineOut && q >= 1)   // this layer's tiles 2q-2, 2q-1 -> the next layer's k-steps
 #pragma unroll
           for (int c = 0; c < kCols; ++c)
             convert_half<kDensityOut>(acc[c][2 * q - 2 + t], half, bout[c][2 * (2 * q - 2 + t) + half], dens[c], cx,
                                       2 * q - 2 + t);
       }
-#endif
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int t = m >> 3, pr = m & 7;
+        if (kConvert && kFineIn && q == 0 && u == dword_unit_in(m))
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) convert_dword(acc[c][6 + t], pr, bh[c][2 * (6 + t) + (pr >> 2)]);
+        if (kConvertOut && kFineOut && q >= 1 && u == dword_unit_out(KU, m))
+#pragma unroll
+          for (int c = 0; c < kCols; ++c)
+            convert_dword(acc[c][2 * q - 2 + t], pr, bout[c][2 * (2 * q - 2 + t) + (pr >> 2)]);
+      }
       after_unit(cx, n);
     }
   }
@@ -530,6 +513,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   __syncthreads();
   NERF_STAMP(cx, 1);
   bf16x8 ra[kRing][2], rb[kRing][kCols];
+  f32x16 acc[kCols][8];
 #pragma unroll
   for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
 #else
@@ -543,13 +527,11 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   stage_chunk(blob, kAhead, lds, wave_u, lane);   // the start of chunk 0
 #endif
 
-  f32x16 acc[kCols][8];
   float dens[kCols];
 #pragma unroll
   for (int c = 0; c < kCols; ++c) dens[c] = 0.0f;
-#ifndef NERF_BF16_LATE_CVT
   // two B-fragment sets: layer l reads one while it fills the other for l+1
-  bf16x8 bA[kCols][16], bB[kCols][16];
+  u32x4 bA[kCols][16], bB[kCols][16];
   layer_bf16<L0>(acc, bB, bA, ra, rb, dens, cx);
   layer_bf16<L1>(acc, bA, bB, ra, rb, dens, cx);
   layer_bf16<L2>(acc, bB, bA, ra, rb, dens, cx);
@@ -559,18 +541,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   layer_bf16<L6>(acc, bB, bA, ra, rb, dens, cx);
   layer_bf16<L7>(acc, bA, bB, ra, rb, dens, cx);
   layer_bf16<C0>(acc, bB, bA, ra, rb, dens, cx);   // [x, PE4(d)] (nerf.py:117-121); density head folded in
-#else
-  bf16x8 bh[kCols][16];
-  layer_bf16<L0>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L1>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L2>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L3>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L4>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L5>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L6>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<L7>(acc, bh, bh, ra, rb, dens, cx);
-  layer_bf16<C0>(acc, bh, bh, ra, rb, dens, cx);
-#endif
+
   const float* prm = (const float*)(lds + kLdsParamOff);
 #pragma unroll
   for (int c = 0; c < kCols; ++c) {

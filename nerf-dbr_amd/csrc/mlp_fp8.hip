@@ -141,7 +141,14 @@ __device__ __forceinline__ float i2f(int x) { return __builtin_bit_cast(float, x
 
 // Four e4m3 bytes from four fp32 values x / s (RNE), low byte first.
 __device__ __forceinline__ int cvt4_scaled(float a, float b, float c, float d, float s) {
+#ifdef NERF_FP8_SEED
+  // the low-word convert preserves the high word, which the second convert
+  // overwrites: seed it with the bits of b (dying here) so the tied destination
+  // takes b's register instead of a copy of a zero
+  i16x2 w = __builtin_bit_cast(i16x2, b);
+#else
   i16x2 w = {0, 0};
+#endif
   w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, a, b, s, false);
   w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, c, d, s, true);
   return __builtin_bit_cast(int, w);
