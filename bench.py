@@ -136,13 +136,10 @@ def main():
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world, local, dev = D.init_from_env()       # RCCL process group when world > 1
+    local = dev
 
     width, height, spp = args.width, args.height, args.spp
     ckpt_dir = tempfile.mkdtemp(prefix=f"nerf_bench_r{rank}_")
@@ -178,11 +175,7 @@ def main():
         step()
         mlp_ms.append(r.hip.stage_ms()["fine_mlp"])
     barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.reduce_max(time.perf_counter() - t0)   # max over ranks
     ms_step = 1000.0 * elapsed / args.steps
     value = width * height * args.steps / elapsed
 
@@ -245,7 +238,9 @@ def main():
             "data": "synthetic: conditioned random-init NeRFModel weights (numpy seed 0), suite pose view 0",
             "config": {"workload": f"render_image {width}x{height}, {spp} uniform samples/ray, fine net",
                        "resolution": [width, height], "samples_per_ray": spp,
-                       "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
+                       "parallelism": (f"row-band x{world} + "
+                                       f"{'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all-gather"
+                                       if world > 1 else "1 GPU")},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_ms,

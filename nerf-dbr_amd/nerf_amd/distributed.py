@@ -41,11 +41,55 @@ def gather_bands(rgb_band, depth_band, width: int, height: int, group=None):
     packed[: r1 - r0, :, :3] = rgb_band
     packed[: r1 - r0, :, 3] = depth_band
     full = torch.empty(world * rows, width, 4, dtype=torch.float32, device=rgb_band.device)
-    dist.all_gather_into_tensor(full, packed, group=group)
+    if packed.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal of the multi-rank path on one device (gloo has no device
+        # all-gather): stage through host memory
+        host = torch.empty(world * rows, width, 4, dtype=torch.float32)
+        dist.all_gather_into_tensor(host, packed.cpu(), group=group)
+        full.copy_(host)
+    else:
+        dist.all_gather_into_tensor(full, packed, group=group)
     full = full.reshape(world, rows, width, 4)
     pieces = [full[r, : b1 - b0] for r, (b0, b1) in enumerate(bands(world, height))]
     img = torch.cat(pieces, 0)
     return img[..., :3].contiguous(), img[..., 3].contiguous()
+
+
+def init_from_env():
+    """(rank, world, local, device index) from torchrun's environment; joins the
+    process group when world > 1.  Backend RCCL ("nccl") unless NERF_DIST_BACKEND
+    says otherwise (gloo: the one-device rehearsal, ranks sharing device
+    local % device_count)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if world > 1:
+        backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local, dev
+
+
+def reduce_max(x: float) -> float:
+    """Max over ranks of a host float (the bench's max-over-ranks time)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return x
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def render_sharded(render_rows: Callable, camera_pose, resolution: Tuple[int, int], samples_per_ray: int,

@@ -1,0 +1,45 @@
+"""Multi-rank render check, launched by tests/test_gpu_parity.py under torchrun.
+
+Every rank renders its row band (nerf_amd.distributed.band) and the bands are
+all-gathered; rank 0 compares the gathered frame with a single-call full-frame
+render (bit-identical expected: rays are independent) and prints one JSON line.
+Backend from NERF_DIST_BACKEND (the test uses gloo so that two ranks can share
+one device; the 8-GPU bench uses RCCL).
+"""
+import json
+import os
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "nerf-dbr_amd")]
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    from nerf_amd import distributed as D
+    from nerf_amd import weights as W
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    rank, world, _, dev = D.init_from_env()
+    ckpt = W.write_synthetic_checkpoint(os.path.join(tempfile.mkdtemp(), "ckpt.pth"), seed=0)
+    r = MI355XRenderer(os.environ.get("NERF_CHECK_PRECISION", "bf16"), device_index=dev)
+    r.setup(ckpt)
+    pose = torch.eye(4)
+    pose[2, 3] = 4.0
+    w, h, s = 96, 37, 32                       # 37 rows: uneven bands
+    rgb, depth = D.render_sharded(r.render_rows, pose, (w, h), s)
+    ok = None
+    if rank == 0:
+        ref_rgb, ref_depth = r.render_image(pose, (w, h), s)
+        ok = bool(torch.equal(rgb, ref_rgb) and torch.equal(depth, ref_depth))
+        print(json.dumps({"world": world, "bands": D.bands(world, h), "identical": ok}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0 if rank != 0 or ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -399,3 +399,40 @@ def test_plain_c_host_matches_python(r32, tmp_path):
     rgb, depth = r32.render_image(pose, (w, h), s)
     assert np.array_equal(out[: w * h * 3], rgb.cpu().numpy().ravel())
     assert np.array_equal(out[w * h * 3:], depth.cpu().numpy().ravel())
+
+
+def _torchrun(args, env_extra, timeout=300):
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, **env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def test_multi_rank_rehearsal_on_one_device():
+    """The N>1 path (bands, all-gather, barrier, max-over-ranks timing, one JSON
+    line from rank 0) with two ranks sharing this box's one GPU over gloo; the
+    driver's multi-GPU bench runs the same code over RCCL."""
+    import json as js
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = _torchrun([os.path.join(repo, "tests", "dist_render_check.py")], {"NERF_DIST_BACKEND": "gloo"})
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = [l for l in res.stdout.splitlines() if l.startswith("{")][-1]
+    out = js.loads(line)
+    assert out["world"] == 2 and out["identical"]
+    res = _torchrun([os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--width", "200",
+                     "--height", "150", "--spp", "32", "--cpu-seconds", "0", "--no-error-check", "--no-extras"],
+                    {"NERF_DIST_BACKEND": "gloo"})
+    assert res.returncode == 0, res.stderr[-3000:]
+    # exactly one JSON line, from rank 0 (gloo's own connection messages aside)
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    b = js.loads(lines[0])
+    assert b["n_gpus"] == 2 and b["value"] > 0 and b["config"]["parallelism"].startswith("row-band x2")
