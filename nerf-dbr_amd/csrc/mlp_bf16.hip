@@ -4,8 +4,10 @@
 // Replaces NeRFModel.forward (src/models/nerf.py:92-131) fused with
 // sample_points_on_rays (src/benchmark/base_renderer.py:260-281) and the
 // positional encoding (nerf.py:24-45).  Activations and weights are rounded to
-// bf16 (RNE) at MFMA inputs; accumulation, bias, ReLU, the density/colour heads
-// and everything outside the MLP stay fp32.
+// bf16 (RNE) at MFMA inputs; accumulation, bias, ReLU and everything outside the
+// MLP stay fp32.  The density and colour heads run on the MFMA too, as one extra
+// 32-row tile after C0 (nerf_layout.h kHeadUnits): their fp32 VALU form was
+// ~450 instructions per wave, and this kernel's time tracks its VALU count.
 //
 // Geometry: 512-thread workgroups of 256 samples, 8 waves (two per SIMD), each
 // owning one 32-sample column tile.  A lane keeps one layer's 8 accumulator
@@ -60,7 +62,7 @@ constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
 #ifndef NERF_BF16_PF
 #define NERF_BF16_PF 2               // fragment prefetch distance (units)
 #endif
-constexpr int kUnits = bf16_unit_base(kNumMfmaLayers);                // 516
+constexpr int kUnits = kHeadUnitBase + kHeadUnits;                   // 516 layer units + 12 head units
 constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitBytes;
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
@@ -96,8 +98,10 @@ NL_HD int unit_layer(int n) {
   while (l + 1 < kNumMfmaLayers && bf16_unit_base(l + 1) <= n) ++l;
   return l;
 }
+NL_HD bool unit_is_head(int n) { return n >= kHeadUnitBase; }
 NL_HD int unit_kstep(int n) { return (n - bf16_unit_base(unit_layer(n))) % ksteps_bf16(unit_layer(n)); }
-NL_HD int unit_extra(int n) {   // 0: B from hidden fragments; else the Extra kind
+NL_HD int unit_extra(int n) {   // 0: B from hidden fragments (or head units); else the Extra kind
+  if (unit_is_head(n)) return 0;
   const int l = unit_layer(n);
   return unit_kstep(n) < layer_shape(l).hidden / 16 ? 0 : layer_shape(l).extra;
 }
@@ -192,23 +196,6 @@ struct Ctx {
   unsigned ring_addr, pe_addr, de_addr, bias_addr;
 };
 
-// Half a tile (registers 8s..8s+7 = k-step 2t+s of the next layer), for the
-// spread schedule below.
-template <bool kDensity>
-__device__ __forceinline__ void convert_half(const f32x16& acc_t, int s, u32x4& b, float& dens, const Ctx& cx, int t) {
-  b = __builtin_bit_cast(u32x4, pack8_relu(acc_t, 8 * s));
-  if (kDensity) {
-    const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
-#pragma unroll
-    for (int q = 2 * s; q < 2 * s + 2; ++q) {
-      const f32x4 w = w4[q];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dens = fmaf(w[i], relu(acc_t[4 * q + i]), dens);
-    }
-    asm volatile("" : "+v"(dens));
-  }
-}
-
 #ifndef NERF_BF16_CC_LDS
 // ---- LDS fragment reads from inline asm with counted waits.  Left to itself
 // hipcc puts an s_waitcnt in front of almost every MFMA (one per fragment);
@@ -222,6 +209,7 @@ NL_HD int unit_reads(int n) { return n < 0 || n >= kUnits ? 0 : 2 + (unit_extra(
 // Issue order per unit body m: [bias reads if m opens a quarter], reads of unit
 // m+kPf, wait, MFMAs of unit m (the prologue issued units 0..kPf-1).
 NL_HD bool unit_opens_quarter(int n) {
+  if (unit_is_head(n)) return false;
   const int l = unit_layer(n);
   return (n - bf16_unit_base(l)) % ksteps_bf16(l) == 0;
 }
@@ -366,18 +354,17 @@ __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (
 
 template <int L>
 __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[kCols][16], u32x4 (&bout)[kCols][16],
-                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], float (&dens)[kCols],
-                                           const Ctx& cx) {
+                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], const Ctx& cx) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
   constexpr int KU = ksteps_bf16(L);
   constexpr int NQ = out_tiles(L) / 2;
   constexpr int N0 = bf16_unit_base(L);
   constexpr bool kConvert = L != L0;          // B fragments come from the previous layer
-  constexpr bool kDensity = L == C0;          // ... which, before C0, also feeds the density head
   [[maybe_unused]] const float* prm = (const float*)(cx.lds + kLdsParamOff);
-  constexpr bool kConvertOut = L != C0;       // this layer's outputs feed another MFMA layer
-  constexpr bool kDensityOut = L == L7;
+  // outputs feed another MFMA layer: the next layer, or (C0) the heads' tile;
+  // C0 has two quarters, so its tiles 2, 3 are converted in the head loop
+  constexpr bool kConvertOut = true;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
 #ifdef NERF_BF16_CC_LDS
@@ -421,32 +408,13 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
         for (int c = 0; c < kCols; ++c)
           acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][o2], b[c], acc[c][2 * q + o2],
                                                                       0, 0, 0);
-#ifndef NERF_BF16_HALF_SLICES
-      constexpr bool kFineIn = !kDensity, kFineOut = !kDensityOut;
-#else
-      constexpr bool kFineIn = false, kFineOut = false;
-#endif
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (u != slice_pos(KU, j)) continue;
-        const int t = j >> 1, half = j & 1;
-        if (kConvert && !kFineIn && q == 0)       // previous layer's tiles 6, 7 -> this layer's k-steps 12..15
-#pragma unroll
-          for (int c = 0; c < kCols; ++c)
-            convert_half<kDensity>(acc[c][6 + t], half, bh[c][2 * (6 + t) + half], dens[c], cx, 6 + t);
-        if (kConvertOut && !kFineOut && q >= 1)   // this layer's tiles 2q-2, 2q-1 -> the next layer's k-steps
-#pragma unroll
-          for (int c = 0; c < kCols; ++c)
-            convert_half<kDensityOut>(acc[c][2 * q - 2 + t], half, bout[c][2 * (2 * q - 2 + t) + half], dens[c], cx,
-                                      2 * q - 2 + t);
-      }
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
-        if (kConvert && kFineIn && q == 0 && u == dword_unit_in(m))
+        if (kConvert && q == 0 && u == dword_unit_in(m))
 #pragma unroll
           for (int c = 0; c < kCols; ++c) convert_dword(acc[c][6 + t], pr, bh[c][2 * (6 + t) + (pr >> 2)]);
-        if (kConvertOut && kFineOut && q >= 1 && u == dword_unit_out(KU, m))
+        if (kConvertOut && q >= 1 && u == dword_unit_out(KU, m))
 #pragma unroll
           for (int c = 0; c < kCols; ++c)
             convert_dword(acc[c][2 * q - 2 + t], pr, bout[c][2 * (2 * q - 2 + t) + (pr >> 2)]);
@@ -527,30 +495,67 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   stage_chunk(blob, kAhead, lds, wave_u, lane);   // the start of chunk 0
 #endif
 
-  float dens[kCols];
-#pragma unroll
-  for (int c = 0; c < kCols; ++c) dens[c] = 0.0f;
   // two B-fragment sets: layer l reads one while it fills the other for l+1
   u32x4 bA[kCols][16], bB[kCols][16];
-  layer_bf16<L0>(acc, bB, bA, ra, rb, dens, cx);
-  layer_bf16<L1>(acc, bA, bB, ra, rb, dens, cx);
-  layer_bf16<L2>(acc, bB, bA, ra, rb, dens, cx);
-  layer_bf16<L3>(acc, bA, bB, ra, rb, dens, cx);
-  layer_bf16<L4>(acc, bB, bA, ra, rb, dens, cx);   // skip: [x, pe] (nerf.py:109-110)
-  layer_bf16<L5>(acc, bA, bB, ra, rb, dens, cx);
-  layer_bf16<L6>(acc, bB, bA, ra, rb, dens, cx);
-  layer_bf16<L7>(acc, bA, bB, ra, rb, dens, cx);
-  layer_bf16<C0>(acc, bB, bA, ra, rb, dens, cx);   // [x, PE4(d)] (nerf.py:117-121); density head folded in
+  layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
+  layer_bf16<L1>(acc, bA, bB, ra, rb, cx);
+  layer_bf16<L2>(acc, bB, bA, ra, rb, cx);
+  layer_bf16<L3>(acc, bA, bB, ra, rb, cx);
+  layer_bf16<L4>(acc, bB, bA, ra, rb, cx);   // skip: [x, pe] (nerf.py:109-110)
+  layer_bf16<L5>(acc, bA, bB, ra, rb, cx);
+  layer_bf16<L6>(acc, bB, bA, ra, rb, cx);
+  layer_bf16<L7>(acc, bA, bB, ra, rb, cx);
+  layer_bf16<C0>(acc, bB, bA, ra, rb, cx);   // [x, PE4(d)] (nerf.py:117-121)
 
+  // Heads (nerf.py:114, 123-129) as one MFMA tile: rows 0-2 colour, row 3
+  // density; k-steps 0..15 over L7's fragments (bB, C0's input), 16..23 over
+  // C0's output (bA[0..3] converted in C0's quarter 1, bA[4..7] below).
   const float* prm = (const float*)(lds + kLdsParamOff);
+  f32x16 hacc[kCols];
 #pragma unroll
   for (int c = 0; c < kCols; ++c) {
-    const float sigma = relu(dens[c] + __shfl_xor(dens[c], 32) + prm[kSigB]);
-    relu_tiles<4>(acc[c]);
-    float rgb[3];
-    color_head(acc[c], prm, h, rgb);
+    hacc[c] = f32x16{};
+    if (h == 0) {
+      hacc[c][0] = prm[kC1B];
+      hacc[c][1] = prm[kC1B + 1];
+      hacc[c][2] = prm[kC1B + 2];
+      hacc[c][3] = prm[kSigB];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kHeadUnits; ++i) {
+    const int n = kHeadUnitBase + i;
+    seam_before(cx, n);
+#ifndef NERF_BF16_CC_LDS
+    if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+    // head units read two fragments each and no bias: the younger reads are
+    // those of the next min(kPf, units left) units (spelled out so it folds)
+    wait_lgkm(2 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
+#else
+    if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int k = 2 * i + s2;
+#pragma unroll
+      for (int c = 0; c < kCols; ++c) {
+        const bf16x8 b = __builtin_bit_cast(bf16x8, k < 16 ? bB[c][k < 16 ? k : 0] : bA[c][k >= 16 ? k - 16 : 0]);
+        hacc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][s2], b, hacc[c], 0, 0, 0);
+      }
+    }
+    // C0's tiles 2, 3 -> colour k-steps 20..23 (bA[4..7]), two dwords per unit
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+      if (i < 8 && m / 2 == i)
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) convert_dword(acc[c][2 + (m >> 3)], m & 7, bA[c][2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
+  }
+#pragma unroll
+  for (int c = 0; c < kCols; ++c) {
     const long p = p0 + c * kSamplesPerWave;
-    if (p < n_points && h == 0) out[p] = f32x4{sigma, rgb[0], rgb[1], rgb[2]};
+    if (p < n_points && h == 0)
+      out[p] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
   }
 #ifdef NERF_STAMPS
   NERF_STAMP(cx, kStampSlots - 1);

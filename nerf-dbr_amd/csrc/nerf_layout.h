@@ -140,9 +140,30 @@ NL_HD int f32_blob_floats() {
 NL_HD int bf16_blob_chunks() {
   return (bf16_unit_base(kNumMfmaLayers) + kUnitsPerChunk - 1) / kUnitsPerChunk;
 }
+// Output heads of the bf16 path on the MFMA (one 32-row tile): rows 0-2 the
+// colour-1 layer (nerf.py:123-127) over C0's 128 outputs, row 3 the density
+// head (nerf.py:114) over L7's 256 outputs, other rows zero.  24 k-steps of 16:
+// k-steps 0..15 density (the L7 fragments C0 also reads), 16..23 colour (C0's
+// output as bf16 fragments, hid_bf16_feature order).  Streamed after C0 as 12
+// units of two k-steps each: unit i = [k-step 2i][lane 64][8 bf16],
+// [k-step 2i+1][lane 64][8 bf16].
+constexpr int kHeadKsteps = 24;
+constexpr int kHeadUnits = kHeadKsteps / 2;
+constexpr int kHeadUnitBase = bf16_unit_base(kNumMfmaLayers);           // 516
+NL_HD int head_k_row_col(int u, int row, int h, int j, int* spec_is_density) {
+  // returns the input feature the (k-step u, row, half h, element j) weight
+  // multiplies, or -1 for a zero weight; *spec_is_density selects the tensor
+  if (u < 16) {
+    *spec_is_density = 1;
+    return row == 3 ? hid_bf16_feature(u, h, j) : -1;
+  }
+  *spec_is_density = 0;
+  return row < 3 ? hid_bf16_feature(u - 16, h, j) : -1;
+}
+
 // Packed bf16 blob size: units rounded up to a multiple of 32 (zero padding),
 // so any kernel chunk geometry of up to 32 units reads inside the buffer.
-constexpr int kBf16BlobBytes = ((bf16_unit_base(kNumMfmaLayers) + 31) / 32) * 32 * kUnitBytes;
+constexpr int kBf16BlobBytes = ((kHeadUnitBase + kHeadUnits + 31) / 32) * 32 * kUnitBytes;
 
 // ------------------------------------------------------------------ fp8 --
 // v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 A and B (OCP e4m3fn).  Lane half h

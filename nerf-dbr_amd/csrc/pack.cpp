@@ -146,6 +146,15 @@ extern "C" int nerf_pack_weights(const float* const* params, int n_params, float
                 *dst++ = col < 0 ? uint16_t(0) : f32_to_bf16_rne(W(spec, row, col));
               }
     }
+    // the heads' tile (nerf_layout.h kHeadUnits)
+    for (int u = 0; u < kHeadKsteps; ++u)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          int dens = 0;
+          const int row = lane & 31;
+          const int f = head_k_row_col(u, row, lane >> 5, j, &dens);
+          *dst++ = f < 0 ? uint16_t(0) : f32_to_bf16_rne(dens ? W(kSpecDensity, 0, f) : W(kSpecColor1, row, f));
+        }
     uint16_t* end = bf16_blob + size_t(kBf16BlobBytes) / 2;
     while (dst < end) *dst++ = 0;
   }

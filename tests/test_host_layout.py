@@ -171,7 +171,24 @@ def emulate(f32_blob, bf16_blob, prm, pe, dpe, precision):
         if li == 7:
             x7 = acc
         x = acc
-    sigma, rgb = heads(prm, x7, x)
+    if precision == "fp32":
+        return heads(prm, x7, x)
+    # bf16: the heads run as one MFMA tile from the head units (nerf_layout.h)
+    raw = bf16_blob[516 * 1024: (516 + 12) * 1024]
+    a = bf16_to_f32(raw).reshape(24, 2, 32, 8)                      # [k-step][half][row][j]
+    x7r, xr = round_bf16(x7), round_bf16(x)
+    out = np.zeros((4, n))
+    for u in range(24):
+        for h in range(2):
+            for j in range(8):
+                if u < 16:
+                    b = x7r[32 * (u >> 1) + 16 * (u & 1) + 8 * (j >> 2) + 4 * h + (j & 3)]
+                else:
+                    v = u - 16
+                    b = xr[32 * (v >> 1) + 16 * (v & 1) + 8 * (j >> 2) + 4 * h + (j & 3)]
+                out += np.outer(a[u, h, :4, j], b)
+    sigma = np.maximum(out[3] + prm[2560], 0)
+    rgb = 1 / (1 + np.exp(-(out[:3] + prm[2948:2951, None])))
     return sigma, rgb
 
 
@@ -182,10 +199,11 @@ def direct(sd, pe, dpe, rnd):
         if i == 4:
             x = np.concatenate([x, pe])
         x = np.maximum(rnd(sd[f"layers.{i}.weight"]).astype(np.float64) @ rnd(x) + sd[f"layers.{i}.bias"][:, None], 0)
-    sigma = np.maximum(sd["density_head.weight"].astype(np.float64) @ x + sd["density_head.bias"][:, None], 0)[0]
+    sigma = np.maximum(rnd(sd["density_head.weight"]).astype(np.float64) @ rnd(x) + sd["density_head.bias"][:, None], 0)[0]
     hcol = np.maximum(rnd(sd["color_layers.0.weight"]).astype(np.float64) @ rnd(np.concatenate([x, dpe]))
                       + sd["color_layers.0.bias"][:, None], 0)
-    rgb = 1 / (1 + np.exp(-(sd["color_layers.1.weight"].astype(np.float64) @ hcol + sd["color_layers.1.bias"][:, None])))
+    rgb = 1 / (1 + np.exp(-(rnd(sd["color_layers.1.weight"]).astype(np.float64) @ rnd(hcol)
+                            + sd["color_layers.1.bias"][:, None])))
     return sigma, rgb
 
 
