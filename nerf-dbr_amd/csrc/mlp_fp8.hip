@@ -22,8 +22,10 @@
 //     layer boundary;
 //   * encodings are e4m3 at scale 1 (|sin|,|cos| <= 1; positions clamped to
 //     +-448).
-// Bias, ReLU, the density and colour heads and everything outside the MLP stay
-// fp32.
+//   * heads as one more MFMA tile (nerf_layout.h kFp8HeadUnits): the density
+//     row in fp8 over C0's own input fragments, the colour rows in bf16 over
+//     C0's output converted to bf16 fragments.
+// Bias, ReLU and everything outside the MLP stay fp32.
 #include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
@@ -35,12 +37,16 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;           // 256
 constexpr int kUnitB = kFp8UnitBytes;                                // 4 KiB: 2 tiles x 64 lanes x 32 B
-constexpr int kUnits = kFp8Units;                                    // 130
+constexpr int kUnits = kFp8Units + kFp8HeadUnits;                    // 134
 constexpr int kChunkUnits = 4;
 constexpr int kChunkB = kChunkUnits * kUnitB;                        // 16 KiB
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
@@ -56,9 +62,12 @@ constexpr int kLdsPeOff = kLdsScaleOff + kFp8ScaleBytes;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * 2048;
 constexpr int kLdsBytes = kLdsDeOff + kWaves * 2048;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+constexpr int kDeFromPe = kLdsDeOff - kLdsPeOff;                      // one address VGPR for both encodings
+static_assert(kDeFromPe + 1024 + 16 <= 65536, "direction reads fit the ds_read offset field");
 static_assert(kFp8ScaleBytes % 16 == 0 && kLdsScaleOff % 16 == 0, "16-B aligned carve");
 
-// ---- compile-time unit map ----
+// ---- compile-time unit map (units kFp8Units.. are the heads') ----
+NL_HD bool unit_is_head(int n) { return n >= kFp8Units; }
 NL_HD int unit_layer(int n) {
   int l = 0;
   while (l + 1 < kNumMfmaLayers && fp8_unit_base(l + 1) <= n) ++l;
@@ -66,17 +75,22 @@ NL_HD int unit_layer(int n) {
 }
 NL_HD int unit_kstep(int n) { return (n - fp8_unit_base(unit_layer(n))) % ksteps_fp8(unit_layer(n)); }
 NL_HD int unit_extra(int n) {
+  if (unit_is_head(n)) return 0;
   const int l = unit_layer(n);
   return unit_kstep(n) < layer_shape(l).hidden / 64 ? 0 : layer_shape(l).extra;
 }
-NL_HD bool unit_opens_quarter(int n) { return unit_kstep(n) == 0; }
+NL_HD bool unit_opens_quarter(int n) { return !unit_is_head(n) && unit_kstep(n) == 0; }
 NL_HD int unit_reads(int n) { return n < 0 || n >= kUnits ? 0 : 4 + (unit_extra(n) != 0 ? 2 : 0); }
 constexpr int kQuarterReads = 8 + 1;          // bias (2 tiles x 4 x 16 B) + the weight-scale pair
-NL_HD int quarter_reads(int m) { return m >= 0 && m < kUnits && unit_opens_quarter(m) ? kQuarterReads : 0; }
-// Issue order per unit body m: [bias + scale reads if m opens a quarter],
-// reads of unit m+kPf, wait, MFMAs.  LDS reads younger than all unit n needs:
+// the reads a unit body issues before its prefetch: a quarter's bias and weight
+// scales, or the density row's scale at the first head unit
+NL_HD int quarter_reads(int m) {
+  return m >= 0 && m < kUnits && unit_opens_quarter(m) ? kQuarterReads : (m == kFp8Units ? 1 : 0);
+}
+// Issue order per unit body m: [quarter_reads(m)], reads of unit m+kPf, wait,
+// MFMAs.  LDS reads younger than all unit n needs:
 NL_HD int lgkm_for_unit(int n) {
-  if (unit_opens_quarter(n)) return unit_reads(n + kPf);
+  if (quarter_reads(n) > 0) return unit_reads(n + kPf);
   int c = 0;
   for (int k = n + 1; k <= n + kPf; ++k) c += unit_reads(k);
   for (int m = n - kPf + 1; m <= n; ++m) c += quarter_reads(m);
@@ -87,7 +101,7 @@ struct Ctx {
   const char* blob;
   char* lds;
   int wave_u, lane, h;
-  unsigned ring_addr, pe_addr, de_addr, bias_addr, scale_addr;
+  unsigned ring_addr, pe_addr, bias_addr, scale_addr;   // direction slots: pe_addr + kDeFromPe
 };
 
 __device__ __forceinline__ void stage_chunk(const Ctx& cx, int g) {
@@ -128,8 +142,8 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRin
                              ds_read_b128<i32x4>(cx.ring_addr, off + o2 * 2048 + 1024));
   const int ex = unit_extra(n);
   if (ex != 0) {
-    const unsigned base = ex == kPos ? cx.pe_addr : cx.de_addr;
-    rb[n % kRing] = join(ds_read_b128<i32x4>(base, 0), ds_read_b128<i32x4>(base, 1024));
+    const int eo = ex == kPos ? 0 : kDeFromPe;
+    rb[n % kRing] = join(ds_read_b128<i32x4>(cx.pe_addr, eo), ds_read_b128<i32x4>(cx.pe_addr, eo + 1024));
   }
 }
 
@@ -141,13 +155,13 @@ __device__ __forceinline__ float i2f(int x) { return __builtin_bit_cast(float, x
 
 // Four e4m3 bytes from four fp32 values x / s (RNE), low byte first.
 __device__ __forceinline__ int cvt4_scaled(float a, float b, float c, float d, float s) {
-#ifdef NERF_FP8_SEED
+#ifdef NERF_FP8_ZERO_SEED
+  i16x2 w = {0, 0};
+#else
   // the low-word convert preserves the high word, which the second convert
   // overwrites: seed it with the bits of b (dying here) so the tied destination
   // takes b's register instead of a copy of a zero
   i16x2 w = __builtin_bit_cast(i16x2, b);
-#else
-  i16x2 w = {0, 0};
 #endif
   w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, a, b, s, false);
   w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, c, d, s, true);
@@ -158,15 +172,23 @@ __device__ __forceinline__ int cvt4(float a, float b, float c, float d) {
   return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
 }
 
+// ReLU on four packed e4m3 bytes: a byte whose sign bit is set (a negative
+// value, -0, or a negative NaN) becomes 0x00 -- the same byte ReLU-then-convert
+// gives, since every non-negative input converts to a byte with the sign clear.
+// The mask is built by v_perm_b32, whose selectors 8..11 replicate the sign
+// bits of bytes 1, 3, 5, 7 of {S0, S1}: with S1 = w and S0 = w << 8 those are
+// the signs of w's bytes 1, 3, 0, 2.
+__device__ __forceinline__ int relu_e4m3x4(int w) {
+  const unsigned mask = __builtin_amdgcn_perm(unsigned(w) << 8, unsigned(w), 0x090B080Au);
+  return int(~mask & unsigned(w));
+}
+
 // Tiles 2u, 2u+1 of the previous layer -> B fragment of hidden k-step u
-// (byte j: register j&15 of tile 2u + (j>>4)), ReLU'd and divided by the
-// sample's activation scale s.  Before C0 the ReLU'd fp32 values also feed the
-// density head (nerf.py:114).
-template <bool kDensity>
-__device__ __forceinline__ void convert_pair(const f32x16& t0, const f32x16& t1, i32x8& b, float s, float& dens,
-                                             const Ctx& cx, int u) {
-  // ReLU on the bit patterns (signed max with 0: negative floats are negative
-  // int32), one v_max_i32 per value and no NaN canonicalising
+// (byte j: register j&15 of tile 2u + (j>>4)), divided by the sample's
+// activation scale s, converted, then ReLU'd on the bytes.
+__device__ __forceinline__ void convert_pair(const f32x16& t0, const f32x16& t1, i32x8& b, float s) {
+#ifdef NERF_FP8_RELU_F32
+  // previous form: ReLU on the fp32 bit patterns, one v_max_i32 per value
   float v[32];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -175,45 +197,56 @@ __device__ __forceinline__ void convert_pair(const f32x16& t0, const f32x16& t1,
   }
 #pragma unroll
   for (int d = 0; d < 8; ++d) b[d] = cvt4_scaled(v[4 * d], v[4 * d + 1], v[4 * d + 2], v[4 * d + 3], s);
-  if (kDensity) {
+#else
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int t = 2 * u + k;
-      const f32x4* w4 = (const f32x4*)(cx.lds + kLdsParamOff + 4 * (kSigW + (cx.h * 8 + t) * 16));
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 w = w4[q];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dens = fmaf(w[i], v[16 * k + 4 * q + i], dens);
-      }
-    }
-    asm volatile("" : "+v"(dens));
+  for (int d = 0; d < 4; ++d) {
+    b[d] = relu_e4m3x4(cvt4_scaled(t0[4 * d], t0[4 * d + 1], t0[4 * d + 2], t0[4 * d + 3], s));
+    b[4 + d] = relu_e4m3x4(cvt4_scaled(t1[4 * d], t1[4 * d + 1], t1[4 * d + 2], t1[4 * d + 3], s));
   }
+#endif
+}
+
+// C0's output -> bf16 B fragments of the colour k-steps (hid_bf16_feature
+// order: k-step k = registers 8(k&1)..+7 of tile k>>1), one dword (two values:
+// v_cvt_pk_bf16_f32, then ReLU as v_pk_max_i16 on the rounded words -- RNE keeps
+// sign and order) per call.  Dword m (0..15) of tiles (t, t+1): tile t + (m>>3),
+// register pair m&7.
+__device__ __forceinline__ unsigned cvt_relu_pair(float lo, float hi) {
+  const bf16x2 p = __builtin_convertvector(f32x2{lo, hi}, bf16x2);
+  const i16x2 m = __builtin_elementwise_max(__builtin_bit_cast(i16x2, p), i16x2(0));
+  return __builtin_bit_cast(unsigned, m);
+}
+__device__ __forceinline__ void colour_dword(const f32x16 (&acc)[8], int t, int m, u32x4 (&hb)[8]) {
+  const int tile = t + (m >> 3), pr = m & 7;
+  hb[2 * tile + (pr >> 2)][pr & 3] = cvt_relu_pair(acc[tile][2 * pr], acc[tile][2 * pr + 1]);
 }
 
 // Running max of ReLU outputs on the fp32 bit patterns: a negative float is a
 // negative int32 and non-negative floats order like their bits, so a signed
 // integer max started at 0 is max(relu(x)) -- v_max3_i32, no NaN canonicalising.
 __device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t1) {
+  // chained as max(max(m, a), b) so each pair folds into one v_max3_i32
 #pragma unroll
   for (int i = 0; i < 16; i += 2)
-    m = __builtin_elementwise_max(m, __builtin_elementwise_max(f2i(t0[i]), f2i(t0[i + 1])));
+    m = __builtin_elementwise_max(__builtin_elementwise_max(m, f2i(t0[i])), f2i(t0[i + 1]));
 #pragma unroll
   for (int i = 0; i < 16; i += 2)
-    m = __builtin_elementwise_max(m, __builtin_elementwise_max(f2i(t1[i]), f2i(t1[i + 1])));
+    m = __builtin_elementwise_max(__builtin_elementwise_max(m, f2i(t1[i])), f2i(t1[i + 1]));
   return m;
 }
 
+// (C0 also leaves its activation scale in sb_out for the density k-steps and
+// converts its tiles 0, 1 to the colour fragments hb[0..3] during quarter 1.)
 template <int L>
 __device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x8 (&ra)[kRing][2],
-                                          i32x8 (&rb)[kRing], int& amax, float& dens, const Ctx& cx) {
+                                          i32x8 (&rb)[kRing], int& amax, int& sb_out, u32x4 (&hb)[8],
+                                          const Ctx& cx) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 64;
   constexpr int KU = ksteps_fp8(L);
   constexpr int NQ = out_tiles(L) / 2;
   constexpr int N0 = fp8_unit_base(L);
   constexpr bool kConvert = L != L0;
-  constexpr bool kDensity = L == C0;
   constexpr bool kNextConverts = L != C0;        // the following layer reads these accumulators
   float s = 1.0f;
   int sb = 127;                                  // E8M0 of the activation scale (1.0 for encodings)
@@ -224,8 +257,9 @@ __device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x
     const int e = __builtin_amdgcn_frexp_expf(i2f(mb)) - 8;   // max = f * 2^(e+8), f in [0.5, 1)
     s = __builtin_ldexpf(1.0f, e);
     sb = 127 + e;
-    convert_pair<kDensity>(acc[0], acc[1], bh[0], s, dens, cx, 0);
+    convert_pair(acc[0], acc[1], bh[0], s);
   }
+  sb_out = sb;
   amax = 0;
   int sa0 = 127, sa1 = 127;
 #pragma unroll
@@ -259,7 +293,12 @@ __device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x
       acc[2 * q + 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][1], b, acc[2 * q + 1], 0, 0, 0,
                                                                       sa1, 0, sbu);
       // conversion slices: tiles (2u+2, 2u+3) -> k-step u+1, before quarter 0 reads it
-      if (kConvert && q == 0 && u < 3) convert_pair<kDensity>(acc[2 * u + 2], acc[2 * u + 3], bh[u + 1], s, dens, cx, u + 1);
+      if (kConvert && q == 0 && u < 3) convert_pair(acc[2 * u + 2], acc[2 * u + 3], bh[u + 1], s);
+      if (L == C0 && q == 1) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if ((m * KU) / 16 == u) colour_dword(acc, 0, m, hb);
+      }
       // running maximum for the next layer's scale: the previous quarter's tiles are final
       if (kNextConverts && q >= 1 && u == (KU > 1 ? 1 : 0)) amax = max_pair(amax, acc[2 * q - 2], acc[2 * q - 1]);
     }
@@ -278,7 +317,6 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   const Ctx cx{blob, lds, wave_u, lane, h,
                base + lane * 16,
                base + kLdsPeOff + wave_u * 2048 + lane * 16,
-               base + kLdsDeOff + wave_u * 2048 + lane * 16,
                base + kLdsParamOff + h * 64,
                base + kLdsScaleOff + lane * 8};
   const long p = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
@@ -320,23 +358,62 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
 
   f32x16 acc[8];
   i32x8 bh[4];
-  int amax = 0;
-  float dens = 0.0f;
-  layer_fp8<L0>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L1>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L2>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L3>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L4>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L5>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L6>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<L7>(acc, bh, ra, rb, amax, dens, cx);
-  layer_fp8<C0>(acc, bh, ra, rb, amax, dens, cx);
+  u32x4 hb[8];
+  int amax = 0, sb = 127;
+  layer_fp8<L0>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L1>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L2>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L3>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L4>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L5>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L6>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<L7>(acc, bh, ra, rb, amax, sb, hb, cx);
+  layer_fp8<C0>(acc, bh, ra, rb, amax, sb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+
+  // Heads (nerf.py:114, 123-129) as one MFMA tile: row 3 density (fp8 k-steps
+  // over bh, C0's input, at C0's activation scale), rows 0-2 colour (bf16
+  // k-steps over hb, C0's output; tiles 2, 3 converted during the density units).
   const float* prm = (const float*)(lds + kLdsParamOff);
-  const float sigma = relu(dens + __shfl_xor(dens, 32) + prm[kSigB]);
-  relu_tiles<4>(acc);
-  float rgb[3];
-  color_head(acc, prm, h, rgb);
-  if (p < n_points && h == 0) out[p] = f32x4{sigma, rgb[0], rgb[1], rgb[2]};
+  f32x16 hacc = f32x16{};
+  if (h == 0) {
+    hacc[0] = prm[kC1B];
+    hacc[1] = prm[kC1B + 1];
+    hacc[2] = prm[kC1B + 2];
+    hacc[3] = prm[kSigB];
+  }
+  int dsa = 127;
+#pragma unroll
+  for (int i = 0; i < kFp8HeadUnits; ++i) {
+    const int n = kFp8Units + i;
+    seam_before(cx, n);
+    if (i == 0) dsa = int(ds_read_b64(cx.scale_addr, (kNumMfmaLayers * 4) * 512)[0]);
+    if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+    wait_lgkm(lgkm_for_unit(n));
+    if (i < kFp8DensityUnits) {
+#pragma unroll
+      for (int o2 = 0; o2 < 2; ++o2)
+        hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
+                                                               0, sb);
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (m / 8 == i) colour_dword(acc, 2, m, hb);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const i32x8 a8 = ra[n % kRing][k >> 1];
+        const i32x4 a4 = (k & 1) ? i32x4{a8[4], a8[5], a8[6], a8[7]} : i32x4{a8[0], a8[1], a8[2], a8[3]};
+        hacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4),
+                                                        __builtin_bit_cast(bf16x8, hb[4 * (i - kFp8DensityUnits) + k]),
+                                                        hacc, 0, 0, 0);
+      }
+    }
+  }
+  // the sample index again, from the lane id recounted by v_mbcnt: keeping the
+  // 64-bit p (or the lane id) live through the layers costs a spill, and its
+  // reload a vmcnt(0) drain of the weight stream
+  const int lane_o = int(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+  const long p_o = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane_o & 31);
+  if (p_o < n_points && h == 0) out[p_o] = f32x4{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
 }
 
 }  // namespace

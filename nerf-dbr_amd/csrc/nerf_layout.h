@@ -197,9 +197,23 @@ NL_HD int fp8_unit_base(int l) {
   return n;
 }
 constexpr int kFp8Units = fp8_unit_base(kNumMfmaLayers);                        // 130
-constexpr int kFp8UnitsPadded = ((kFp8Units + 7) / 8) * 8;                      // 136
+// Heads of the fp8 path: one 32-row tile accumulated by two kinds of MFMA.
+//   * density (row 3, nerf.py:114): 4 fp8 k-steps over L7's output, i.e. C0's
+//     own hidden B fragments and activation scale.  Two units after C0's, laid
+//     out as fp8 units whose o2 is the k-step's parity: unit i holds k-steps
+//     2i (o2 0) and 2i+1 (o2 1), rows other than 3 zero; the row's E8M0 scale
+//     is the scale table's entry for (layer kNumMfmaLayers, quarter 0, o2 0).
+//   * colour (rows 0-2, nerf.py:123-127): 8 bf16 k-steps (v_mfma_f32_32x32x16_bf16)
+//     over C0's output as bf16 fragments (hid_bf16_feature order), 4 per unit:
+//     [k-step][lane 64][8 bf16] -- the same byte offsets as an fp8 unit's
+//     [o2][p][lane][16 B], so the unit reads as (o2, p) = (k>>1, k&1).
+// fp8 colour was measured 30 % worse in mean RGB error than bf16 colour, fp8
+// density no worse than fp32 density (tests/test_host_layout.py notes).
+constexpr int kFp8DensityUnits = 2, kFp8ColourUnits = 2;
+constexpr int kFp8HeadUnits = kFp8DensityUnits + kFp8ColourUnits;
+constexpr int kFp8UnitsPadded = ((kFp8Units + kFp8HeadUnits + 7) / 8) * 8;      // 136
 constexpr int kFp8ScaleOff = kFp8UnitsPadded * kFp8UnitBytes;                   // bytes
-constexpr int kFp8ScaleBytes = kNumMfmaLayers * 4 * 64 * 2 * 4;
+constexpr int kFp8ScaleBytes = (kNumMfmaLayers + 1) * 4 * 64 * 2 * 4;           // + the heads' row
 constexpr int kFp8BlobBytes = kFp8ScaleOff + kFp8ScaleBytes;
 constexpr float kFp8Max = 448.0f;                                              // largest finite e4m3fn
 

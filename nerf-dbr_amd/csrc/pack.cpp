@@ -102,6 +102,31 @@ extern "C" int nerf_pack_weights_fp8(const float* const* params, int n_params, u
                 *dst++ = col < 0 ? uint8_t(0) : f32_to_e4m3_rne(std::ldexp(W(spec, row, col), -exps[row]));
               }
   }
+  // the heads (nerf_layout.h kFp8HeadUnits): density row 3 in fp8 over C0's
+  // hidden k-steps, with its own row scale ...
+  float dmax = 0.0f;
+  for (int k = 0; k < kHidden; ++k) dmax = std::fmax(dmax, std::fabs(W(kSpecDensity, 0, k)));
+  const int de = row_scale_exp(dmax);
+  for (int lane = 0; lane < 64; ++lane)
+    for (int o2 = 0; o2 < 2; ++o2)
+      scales[((kNumMfmaLayers * 4) * 64 + lane) * 2 + o2] = (lane & 31) == 3 ? uint32_t(127 + de) : 127u;
+  for (int i = 0; i < kFp8DensityUnits; ++i)
+    for (int o2 = 0; o2 < 2; ++o2)
+      for (int p = 0; p < 2; ++p)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int jj = 0; jj < 16; ++jj) {
+            const int col = fp8_k_col(C0, 2 * i + o2, lane >> 5, 16 * p + jj);
+            *dst++ = (lane & 31) != 3 || col < 0 ? uint8_t(0)
+                                                  : f32_to_e4m3_rne(std::ldexp(W(kSpecDensity, 0, col), -de));
+          }
+  // ... colour rows 0-2 in bf16 over C0's output
+  uint16_t* hd = reinterpret_cast<uint16_t*>(dst);
+  for (int k = 0; k < 4 * kFp8ColourUnits; ++k)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int j = 0; j < 8; ++j) {
+        const int row = lane & 31;
+        *hd++ = row < 3 ? f32_to_bf16_rne(W(kSpecColor1, row, hid_bf16_feature(k, lane >> 5, j))) : uint16_t(0);
+      }
   return NERF_OK;
 }
 

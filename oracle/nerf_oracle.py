@@ -255,11 +255,20 @@ def render_image_hierarchical(coarse: Net, fine: Net, c2w, resolution: Tuple[int
 #     max|W_r| / 2^e_r <= 448, per output row r;
 #   * activations (previous layer's ReLU output): e4m3 of x / 2^e_s, per sample,
 #     e_s = frexp exponent of the sample's largest value - 8 (range [128, 256));
-#   * encodings: e4m3 at scale 1; bias, heads and accumulation in full precision.
+#   * encodings: e4m3 at scale 1; bias and accumulation in full precision;
+#   * heads (nerf_layout.h kFp8HeadUnits): density as one more fp8 row over C0's
+#     quantised input (its own row scale), colour in bf16 (weights and ReLU'd
+#     C0 outputs rounded to bf16, RNE).
 # Parity for this path is against this restatement, not the reference.
 def e4m3_round(x):
     """f32 -> float8_e4m3fn (round to nearest even) -> float64."""
     t = torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.float8_e4m3fn)
+    return t.float().numpy().astype(np.float64)
+
+
+def bf16_round(x):
+    """f32 -> bfloat16 (round to nearest even) -> float64."""
+    t = torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.bfloat16)
     return t.float().numpy().astype(np.float64)
 
 
@@ -289,10 +298,11 @@ def fp8_mlp_restated(sd, pe, dpe):
         w = fp8_weight_rows(sd[f"layers.{i}.weight"])
         inp = pq if i == 0 else (np.concatenate([aq(x), pq]) if i == 4 else aq(x))
         x = np.maximum(w @ inp + sd[f"layers.{i}.bias"][:, None], 0)
-    sigma = np.maximum(sd["density_head.weight"].astype(np.float64) @ x + sd["density_head.bias"][:, None], 0)[0]
-    hcol = np.maximum(fp8_weight_rows(sd["color_layers.0.weight"]) @ np.concatenate([aq(x), dq])
+    xq = aq(x)
+    sigma = np.maximum(fp8_weight_rows(sd["density_head.weight"]) @ xq + sd["density_head.bias"][:, None], 0)[0]
+    hcol = np.maximum(fp8_weight_rows(sd["color_layers.0.weight"]) @ np.concatenate([xq, dq])
                       + sd["color_layers.0.bias"][:, None], 0)
-    rgb = 1 / (1 + np.exp(-(sd["color_layers.1.weight"].astype(np.float64) @ hcol
+    rgb = 1 / (1 + np.exp(-(bf16_round(sd["color_layers.1.weight"]) @ bf16_round(hcol)
                             + sd["color_layers.1.bias"][:, None])))
     return sigma, rgb
 

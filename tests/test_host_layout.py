@@ -284,9 +284,9 @@ def emulate_fp8(blob, prm, pe, dpe):
     """Kernel lane maps of the fp8 path (nerf_layout.h), float64 accumulation."""
     n = pe.shape[1]
     scale_off = 136 * 4096
-    scales = blob[scale_off:].view(np.uint32).reshape(9, 4, 64, 2)
+    scales = blob[scale_off:].view(np.uint32).reshape(10, 4, 64, 2)
     off = 0
-    x = x7 = None
+    x = xq = None
     for li, (_, out, hidden, extra) in enumerate(LAYERS):
         nt, nq = out // 32, out // 64
         ku = hidden // 64 + (1 if extra else 0)
@@ -316,9 +316,25 @@ def emulate_fp8(blob, prm, pe, dpe):
                             b = ext[h]
                         acc[row] += s * (a[q, u, o2, lane].astype(np.float64) @ b)
         x = np.maximum(acc, 0)
-        if li == 7:
-            x7 = x
-    return heads(prm, x7, x)
+    # heads: density row 3 as 4 fp8 k-steps over C0's quantised input (xq, still
+    # L7's), at the row scale of table entry (9, 0, lane, 0) ...
+    a = e4m3_decode(blob[off: off + 2 * 4096]).reshape(2, 2, 2, 64, 16)
+    a = a.transpose(0, 1, 3, 2, 4).reshape(4, 64, 32)                 # [k-step][lane][byte j]
+    out = np.zeros((4, n))
+    for lane in (3, 35):
+        h = lane >> 5
+        s = np.ldexp(1.0, int(scales[9, 0, lane, 0] & 0xFF) - 127)
+        for u in range(4):
+            b = xq[[32 * (2 * u + (j >> 4)) + acc_row(j & 15, h) for j in range(32)]]
+            out[3] += s * (a[u, lane].astype(np.float64) @ b)
+    # ... colour rows 0-2 as 8 bf16 k-steps over C0's ReLU'd output
+    c = bf16_to_f32(blob[off + 2 * 4096: off + 4 * 4096].view(np.uint16)).reshape(8, 2, 32, 8)   # [k][h][row][j]
+    xr = round_bf16(x)
+    for u in range(8):
+        for h in range(2):
+            for j in range(8):
+                out[:3] += np.outer(c[u, h, :3, j], xr[32 * (u >> 1) + 16 * (u & 1) + 8 * (j >> 2) + 4 * h + (j & 3)])
+    return np.maximum(out[3] + prm[2560], 0), 1 / (1 + np.exp(-(out[:3] + prm[2948:2951, None])))
 
 
 def test_fp8_packing_computes_the_mlp(samples):
@@ -326,7 +342,7 @@ def test_fp8_packing_computes_the_mlp(samples):
     sd = W.synthetic_state_dict(1)
     blob = rt.pack_weights_fp8(sd)
     _, _, prm = rt.pack_weights(sd)
-    assert blob.size == 136 * 4096 + 9 * 4 * 64 * 2 * 4
+    assert blob.size == 136 * 4096 + 10 * 4 * 64 * 2 * 4
     s_emu, rgb_emu = emulate_fp8(blob, prm, pe[:, :6], dpe[:, :6])
     s_dir, rgb_dir = O.fp8_mlp_restated(sd, pe[:, :6], dpe[:, :6])
     np.testing.assert_allclose(s_emu, s_dir, rtol=1e-6, atol=1e-6)
