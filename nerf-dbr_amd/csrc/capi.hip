@@ -21,6 +21,18 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
+int nerf::current_device_cus() {
+  static int cache[64] = {};   // benign race: every writer stores the same value
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 #define HIP_TRY(expr)                                                                                 \
   do {                                                                                                \
     hipError_t e_ = (expr);                                                                           \

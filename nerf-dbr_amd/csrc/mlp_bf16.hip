@@ -25,15 +25,23 @@
 // (see layer_bf16).
 //
 // Weight stream.  The packed blob is a sequence of 2 KiB units (layer, quarter,
-// k-step) cut into 16 KiB chunks.  A 4-slot LDS ring is filled by
+// k-step) cut into 16 KiB chunks.  A 3-slot LDS ring is filled by
 // global_load_lds_dwordx4 (lane-linear 1 KiB pieces, issued from inline asm)
-// three chunks ahead.  One raw s_barrier per chunk, placed where the fragment
+// two chunks ahead.  One raw s_barrier per chunk, placed where the fragment
 // prefetch first reaches into the next chunk, both publishes that chunk (after
-// a counted vmcnt for this wave's own pieces, never 0 in the loop) and frees
-// the slot of the chunk before, which is restaged right away.  Fragments are
-// prefetched two units ahead through a 3-entry register ring; every LDS read
-// in the loop is inline asm, and each unit waits once, with a compile-time
-// lgkmcnt, for exactly the reads its MFMAs consume.
+// a counted vmcnt for this wave's own pieces) and frees the slot of the chunk
+// before, which is restaged right away.  Fragments are prefetched two units
+// ahead through a 3-entry register ring; every LDS read in the loop is inline
+// asm, and each unit waits once, with a compile-time lgkmcnt, for exactly the
+// reads its MFMAs consume.
+//
+// Persistent tiles.  One workgroup per CU loops over 256-sample tiles.  The
+// weight stream never stops: a tile's last seams stage the next tile's first
+// chunks (the stream length is a multiple of the ring, so chunk g always uses
+// slot g % kSlots), so the ring does not refill per tile, the parameters are
+// copied once, and no workgroup launch gap remains.  Each wave re-encodes its
+// own samples into its own LDS slots at the top of a tile; one barrier there
+// publishes chunk 0.
 #include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
@@ -54,10 +62,7 @@ constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
 #define NERF_BF16_CHUNK_UNITS 8      // 2 KiB units per LDS chunk (one barrier per chunk)
 #endif
 #ifndef NERF_BF16_SLOTS
-#define NERF_BF16_SLOTS 4            // chunk slots in the LDS ring
-#endif
-#ifndef NERF_BF16_AHEAD
-#define NERF_BF16_AHEAD 3            // chunks in flight ahead of the one being read
+#define NERF_BF16_SLOTS 3            // chunk slots in the LDS ring (chunks in flight: kSlots - 1)
 #endif
 #ifndef NERF_BF16_PF
 #define NERF_BF16_PF 2               // fragment prefetch distance (units)
@@ -66,13 +71,13 @@ constexpr int kUnits = kHeadUnitBase + kHeadUnits;                   // 516 laye
 constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitBytes;
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
-constexpr int kSlots = NERF_BF16_SLOTS, kAhead = NERF_BF16_AHEAD;
+constexpr int kSlots = NERF_BF16_SLOTS;
 constexpr int kPf = NERF_BF16_PF;
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // LDS-DMA pieces per wave per chunk
 constexpr int kLdsParamOff = kSlots * kChunkB;
-static_assert(kSlots >= kAhead + 1, "a slot is restaged only after every read of its previous chunk");
-static_assert(kAhead >= 2 && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
+static_assert(kSlots >= 3 && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
+static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile: chunk g of every tile uses slot g % kSlots");
 static_assert(kTotalChunks * kChunkB <= kBf16BlobBytes, "device blob is padded for every chunk geometry");
 constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kCols * 4 * 1024;
@@ -170,7 +175,7 @@ __device__ __forceinline__ bf16x8 pack8_relu(const f32x16& a, int base) {
 [[maybe_unused]] constexpr int kStampSlots = 2 + 3 * kTotalChunks + 1;
 #ifdef NERF_STAMPS
 constexpr int kStampBlocks = 256;
-constexpr unsigned kStampFirst = 8192;   // steady state: well past the cold-L2 first wave of blocks
+constexpr long kStampFirst = 8192;       // tiles; steady state: well past the cold-L2 first round
 __device__ unsigned long long g_nerf_stamps[kStampBlocks][kWaves][kStampSlots];
 // shader clock vs the 100 MHz constant clock over each wave's life (clock = dt/drt * 100 MHz)
 __device__ unsigned long long g_nerf_clock[kStampBlocks][kWaves][4];
@@ -258,30 +263,21 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
 #endif
 }
 
-// Chunks whose LDS-DMA may still be in flight after stage(g+2) has landed:
-// stage(g+3 .. g+kAhead), as far as they were issued.
-NL_HD int stages_after(int g) {
-  const int last = (g + kAhead < kTotalChunks - 1) ? g + kAhead : kTotalChunks - 1;
-  return last > g + 2 ? last - (g + 2) : 0;
-}
-
-#ifndef NERF_BF16_SEAM_OLD
 // Seam E_g, at the top of unit n when its prefetch (unit n+kPf) is the first
 // unit of chunk g+1.  Every read of chunk g-1 was consumed by MFMAs of earlier
 // units (so no lgkmcnt wait), so after the barrier its slot is free:
 //   (1) own LDS-DMA pieces of chunk g+1 landed (counted vmcnt; chunk g+1 was
-//       staged kSlots-2 seams earlier),
+//       staged kSlots-2 seams earlier, and kSlots-3 younger stages are in flight),
 //   (2) s_barrier: chunk g+1 is published and every wave is past chunk g-1,
-//   (3) stage chunk g+kSlots-1 into chunk g-1's slot.
-NL_HD int dma_outstanding_at_seam(int g) {   // stages issued but not needed yet at E_g
-  const int issued_last = (g + kSlots - 2 < kTotalChunks - 1) ? g + kSlots - 2 : kTotalChunks - 1;
-  return issued_last > g + 1 ? issued_last - (g + 1) : 0;
-}
+//   (3) stage chunk g+kSlots-1 into chunk g-1's slot -- past the end of the
+//       tile, the next tile's chunk of the same slot.
+// The top of a tile is seam E_-1 (tile_top).
+constexpr int kDmaOutstandingAtSeam = kSlots - 3;
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
   const int g = (n + kPf) / kChunkUnits - 1;
   NERF_STAMP(cx, 2 + 3 * g);
-  wait_vmcnt(kGldsPerStage * dma_outstanding_at_seam(g));
+  wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
   NERF_STAMP(cx, 3 + 3 * g);
 #if !defined(NERF_ABLATE_BARRIER) && !defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no chunk barrier
@@ -289,33 +285,8 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
 #endif
   compiler_fence();
   NERF_STAMP(cx, 4 + 3 * g);
-  if (g + kSlots - 1 < kTotalChunks) stage_chunk(cx.blob, g + kSlots - 1, cx.lds, cx.wave_u, cx.lane);
+  stage_chunk(cx.blob, (g + kSlots - 1) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
 }
-__device__ __forceinline__ void after_unit(const Ctx&, int) {}
-#else
-__device__ __forceinline__ void seam_before(const Ctx&, int) {}
-// After unit n: when it closes chunk g, (1) this wave's reads of slot g are
-// complete (lgkmcnt(0): the slot is restaged after the barrier), (2) its own
-// pieces of chunk g+2 have landed (counted vmcnt), (3) the barrier publishes
-// chunk g+2 to every wave, then (4) chunk g+1+kAhead starts loading into the
-// slot chunk g+1+kAhead-kSlots used.
-__device__ __forceinline__ void after_unit(const Ctx& cx, int n) {
-  if ((n + 1) % kChunkUnits != 0 || n + 1 >= kUnits) return;
-  const int g = n / kChunkUnits;
-  NERF_STAMP(cx, 2 + 3 * g);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  wait_vmcnt(kGldsPerStage * stages_after(g));
-  compiler_fence();
-  NERF_STAMP(cx, 3 + 3 * g);
-#if !defined(NERF_ABLATE_BARRIER) && !defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no chunk barrier
-  __builtin_amdgcn_s_barrier();
-#endif
-  compiler_fence();
-  NERF_STAMP(cx, 4 + 3 * g);
-  if (g + 1 + kAhead < kTotalChunks) stage_chunk(cx.blob, g + 1 + kAhead, cx.lds, cx.wave_u, cx.lane);
-}
-#endif
-
 // Conversion schedule (default): layer L's output tiles 2q-2, 2q-1 become final
 // at the end of its quarter q-1 and are converted to the next layer's B
 // fragments (bout) in four half-tile slices during quarter q = 1..3; tiles 6, 7
@@ -419,8 +390,18 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
           for (int c = 0; c < kCols; ++c)
             convert_dword(acc[c][2 * q - 2 + t], pr, bout[c][2 * (2 * q - 2 + t) + (pr >> 2)]);
       }
-      after_unit(cx, n);
     }
+  }
+}
+
+// (sigma, r, g, b) of a tile's samples; p0 < 0: nothing pending
+__device__ __forceinline__ void store_results(const f32x4 (&res)[kCols], long p0, long n_points, int h,
+                                              f32x4* __restrict__ out) {
+  if (p0 < 0) return;
+#pragma unroll
+  for (int c = 0; c < kCols; ++c) {
+    const long p = p0 + c * kSamplesPerWave;
+    if (p < n_points && h == 0) out[p] = res[c];
   }
 }
 
@@ -433,143 +414,152 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
-  const Ctx cx{blob, lds, wave_u, lane, h, lds_base + lane * 16,
+  const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16,
                lds_base + kLdsPeOff + wave_u * kCols * 4096 + lane * 16,
                lds_base + kLdsDeOff + wave_u * kCols * 2048 + lane * 16,
                lds_base + kLdsParamOff + h * 64};
-  const long p0 = (long(blockIdx.x) * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
-  NERF_STAMP(cx, 0);
-#ifdef NERF_STAMPS
-  const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
+  const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
-  // Kick off the weight stream, then do the per-sample prologue under it.
-#ifndef NERF_BF16_SEAM_OLD
-  constexpr int kPrologueStages = kSlots - 1 < kTotalChunks ? kSlots - 1 : kTotalChunks;
-#else
-  constexpr int kPrologueStages = kAhead;
-#endif
+  // Start the weight stream (chunks 0 .. kSlots-3; each tile's top stages one
+  // more) and copy the parameters, once per workgroup.
 #pragma unroll
-  for (int g = 0; g < kPrologueStages; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
+  const float* prm = (const float*)(lds + kLdsParamOff);
+
+  // A tile's results are stored at the top of the next tile, after its seam:
+  // vmcnt counts stores with the LDS-DMA in issue order, so a store issued last
+  // would make the next tile's first wait also wait out the store.
+  f32x4 res[kCols];
+  long res_p0 = -1;
 
 #pragma unroll 1
-  for (int c = 0; c < kCols; ++c) {
-    const long p = p0 + c * kSamplesPerWave;
-    float x[3], d[3], pef[32], def[16];
-    fetch_sample<kExplicit>(src, p < n_points ? p : n_points - 1, x, d);
+  for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const long p0 = (tile * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
+    // an opaque copy of the stream base per tile: otherwise the 66 chunk
+    // addresses (blob + constant) are hoisted out of the tile loop and held in
+    // SGPRs (spilling); recomputing each is one scalar add pair at its stage
+    Ctx cx = cx0;
+    asm volatile("" : "+s"(cx.blob));
+#ifdef NERF_STAMPS
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    NERF_STAMP(cx, 0);
+    // This tile's encodings, into this wave's own LDS slots (its reads of the
+    // previous tile's were waited for before their MFMAs).
+#pragma unroll 1
+    for (int c = 0; c < kCols; ++c) {
+      const long p = p0 + c * kSamplesPerWave;
+      float x[3], d[3], pef[32], def[16];
+      fetch_sample<kExplicit>(src, p < n_points ? p : n_points - 1, x, d);
 #if defined(NERF_ABLATE_ENCODING) || defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no sin/cos
 #pragma unroll
-    for (int q = 0; q < 32; ++q) pef[q] = x[q % 3] * float(q);
+      for (int q = 0; q < 32; ++q) pef[q] = x[q % 3] * float(q);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) def[q] = d[q % 3] * float(q);
+      for (int q = 0; q < 16; ++q) def[q] = d[q % 3] * float(q);
 #else
-    pos_encode<true>(x[0], x[1], x[2], h, pef);
-    dir_encode<true>(d[0], d[1], d[2], h, def);
+      pos_encode<true>(x[0], x[1], x[2], h, pef);
+      dir_encode<true>(d[0], d[1], d[2], h, def);
 #endif
-    char* pe_dst = lds + kLdsPeOff + (wave_u * kCols + c) * 4096 + lane * 16;
-    char* de_dst = lds + kLdsDeOff + (wave_u * kCols + c) * 2048 + lane * 16;
+      char* pe_dst = lds + kLdsPeOff + (wave_u * kCols + c) * 4096 + lane * 16;
+      char* de_dst = lds + kLdsDeOff + (wave_u * kCols + c) * 2048 + lane * 16;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) *(bf16x8*)(pe_dst + u * 1024) = pack8(pef + 8 * u);
-    *(bf16x8*)(de_dst) = pack8(def);
-    *(bf16x8*)(de_dst + 1024) = pack8(def + 8);
-  }
-#ifndef NERF_BF16_SEAM_OLD
-  // chunk 0 published (later stages may still fly); prime the fragment ring
-  wait_vmcnt(kGldsPerStage * (kPrologueStages - 1));
-  __syncthreads();
-  NERF_STAMP(cx, 1);
-  bf16x8 ra[kRing][2], rb[kRing][kCols];
-  f32x16 acc[kCols][8];
-#pragma unroll
-  for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
-#else
-  // chunks 0 and 1 published (later stages may still fly); prime the fragment ring
-  wait_vmcnt(kGldsPerStage * (kAhead - 2));
-  __syncthreads();
-  NERF_STAMP(cx, 1);
-  bf16x8 ra[kRing][2], rb[kRing][kCols];
-#pragma unroll
-  for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
-  stage_chunk(blob, kAhead, lds, wave_u, lane);   // the start of chunk 0
-#endif
-
-  // two B-fragment sets: layer l reads one while it fills the other for l+1
-  u32x4 bA[kCols][16], bB[kCols][16];
-  layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
-  layer_bf16<L1>(acc, bA, bB, ra, rb, cx);
-  layer_bf16<L2>(acc, bB, bA, ra, rb, cx);
-  layer_bf16<L3>(acc, bA, bB, ra, rb, cx);
-  layer_bf16<L4>(acc, bB, bA, ra, rb, cx);   // skip: [x, pe] (nerf.py:109-110)
-  layer_bf16<L5>(acc, bA, bB, ra, rb, cx);
-  layer_bf16<L6>(acc, bB, bA, ra, rb, cx);
-  layer_bf16<L7>(acc, bA, bB, ra, rb, cx);
-  layer_bf16<C0>(acc, bB, bA, ra, rb, cx);   // [x, PE4(d)] (nerf.py:117-121)
-
-  // Heads (nerf.py:114, 123-129) as one MFMA tile: rows 0-2 colour, row 3
-  // density; k-steps 0..15 over L7's fragments (bB, C0's input), 16..23 over
-  // C0's output (bA[0..3] converted in C0's quarter 1, bA[4..7] below).
-  const float* prm = (const float*)(lds + kLdsParamOff);
-  f32x16 hacc[kCols];
-#pragma unroll
-  for (int c = 0; c < kCols; ++c) {
-    hacc[c] = f32x16{};
-    if (h == 0) {
-      hacc[c][0] = prm[kC1B];
-      hacc[c][1] = prm[kC1B + 1];
-      hacc[c][2] = prm[kC1B + 2];
-      hacc[c][3] = prm[kSigB];
+      for (int u = 0; u < 4; ++u) *(bf16x8*)(pe_dst + u * 1024) = pack8(pef + 8 * u);
+      *(bf16x8*)(de_dst) = pack8(def);
+      *(bf16x8*)(de_dst + 1024) = pack8(def + 8);
     }
-  }
+
+    // Seam E_-1: chunk 0 landed (own pieces) and is published, parameters too
+    // on the first tile; chunk kSlots-2 starts loading into its slot, whose
+    // previous chunk every wave finished with the last tile.
+    wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
+    __syncthreads();
+    stage_chunk(cx.blob, kSlots - 2, lds, wave_u, lane);
+    NERF_STAMP(cx, 1);
+    store_results(res, res_p0, n_points, h, out);
+    bf16x8 ra[kRing][2], rb[kRing][kCols];
+    f32x16 acc[kCols][8];
 #pragma unroll
-  for (int i = 0; i < kHeadUnits; ++i) {
-    const int n = kHeadUnitBase + i;
-    seam_before(cx, n);
-#ifndef NERF_BF16_CC_LDS
-    if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
-    // head units read two fragments each and no bias: the younger reads are
-    // those of the next min(kPf, units left) units (spelled out so it folds)
-    wait_lgkm(2 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
-#else
-    if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
-#endif
-    __builtin_amdgcn_sched_barrier(0);
+    for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+
+    // two B-fragment sets: layer l reads one while it fills the other for l+1
+    u32x4 bA[kCols][16], bB[kCols][16];
+    layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
+    layer_bf16<L1>(acc, bA, bB, ra, rb, cx);
+    layer_bf16<L2>(acc, bB, bA, ra, rb, cx);
+    layer_bf16<L3>(acc, bA, bB, ra, rb, cx);
+    layer_bf16<L4>(acc, bB, bA, ra, rb, cx);   // skip: [x, pe] (nerf.py:109-110)
+    layer_bf16<L5>(acc, bA, bB, ra, rb, cx);
+    layer_bf16<L6>(acc, bB, bA, ra, rb, cx);
+    layer_bf16<L7>(acc, bA, bB, ra, rb, cx);
+    layer_bf16<C0>(acc, bB, bA, ra, rb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+
+    // Heads (nerf.py:114, 123-129) as one MFMA tile: rows 0-2 colour, row 3
+    // density; k-steps 0..15 over L7's fragments (bB, C0's input), 16..23 over
+    // C0's output (bA[0..3] converted in C0's quarter 1, bA[4..7] below).
+    f32x16 hacc[kCols];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int k = 2 * i + s2;
-#pragma unroll
-      for (int c = 0; c < kCols; ++c) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, k < 16 ? bB[c][k < 16 ? k : 0] : bA[c][k >= 16 ? k - 16 : 0]);
-        hacc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][s2], b, hacc[c], 0, 0, 0);
+    for (int c = 0; c < kCols; ++c) {
+      hacc[c] = f32x16{};
+      if (h == 0) {
+        hacc[c][0] = prm[kC1B];
+        hacc[c][1] = prm[kC1B + 1];
+        hacc[c][2] = prm[kC1B + 2];
+        hacc[c][3] = prm[kSigB];
       }
     }
-    // C0's tiles 2, 3 -> colour k-steps 20..23 (bA[4..7]), two dwords per unit
 #pragma unroll
-    for (int m = 0; m < 16; ++m)
-      if (i < 8 && m / 2 == i)
-#pragma unroll
-        for (int c = 0; c < kCols; ++c) convert_dword(acc[c][2 + (m >> 3)], m & 7, bA[c][2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
-  }
-#pragma unroll
-  for (int c = 0; c < kCols; ++c) {
-    const long p = p0 + c * kSamplesPerWave;
-    if (p < n_points && h == 0)
-      out[p] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
-  }
-#ifdef NERF_STAMPS
-  NERF_STAMP(cx, kStampSlots - 1);
-  if (blockIdx.x - kStampFirst < kStampBlocks && lane == 0) {
-    unsigned long long* c = g_nerf_clock[blockIdx.x - kStampFirst][wave_u];
-    c[0] = clk_t0;
-    c[1] = clk_r0;
-    c[2] = __builtin_amdgcn_s_memtime();
-    c[3] = __builtin_amdgcn_s_memrealtime();
-  }
-  if (blockIdx.x - kStampFirst < kStampBlocks && lane == 0)
-    for (int i = 0; i < kStampSlots; ++i)
-      g_nerf_stamps[blockIdx.x - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
+    for (int i = 0; i < kHeadUnits; ++i) {
+      const int n = kHeadUnitBase + i;
+      seam_before(cx, n);
+#ifndef NERF_BF16_CC_LDS
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      // head units read two fragments each and no bias: the younger reads are
+      // those of the next min(kPf, units left) units (spelled out so it folds)
+      wait_lgkm(2 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
+#else
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
 #endif
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int k = 2 * i + s2;
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) {
+          const bf16x8 b = __builtin_bit_cast(bf16x8, k < 16 ? bB[c][k < 16 ? k : 0] : bA[c][k >= 16 ? k - 16 : 0]);
+          hacc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][s2], b, hacc[c], 0, 0, 0);
+        }
+      }
+      // C0's tiles 2, 3 -> colour k-steps 20..23 (bA[4..7]), two dwords per unit
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (i < 8 && m / 2 == i)
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) convert_dword(acc[c][2 + (m >> 3)], m & 7, bA[c][2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
+    }
+#pragma unroll
+    for (int c = 0; c < kCols; ++c)
+      res[c] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
+    res_p0 = p0;
+#ifdef NERF_STAMPS
+    NERF_STAMP(cx, kStampSlots - 1);
+    if (tile - kStampFirst < kStampBlocks && lane == 0) {
+      unsigned long long* c = g_nerf_clock[tile - kStampFirst][wave_u];
+      c[0] = clk_t0;
+      c[1] = clk_r0;
+      c[2] = __builtin_amdgcn_s_memtime();
+      c[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (tile - kStampFirst < kStampBlocks && lane == 0)
+      for (int i = 0; i < kStampSlots; ++i)
+        g_nerf_stamps[tile - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
+#endif
+  }
+  store_results(res, res_p0, n_points, h, out);
+  // the stream ran kSlots-2 chunks into a tile that does not exist: let them
+  // land before the workgroup's LDS is released
+  wait_vmcnt(0);
 }
 
 }  // namespace
@@ -577,7 +567,12 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
                            bool explicit_points, hipStream_t stream) {
   if (n_points <= 0) return hipSuccess;
-  const long blocks = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+#ifdef NERF_BF16_ONE_TILE
+  const long blocks = tiles;                        // lab: one tile per workgroup
+#else
+  const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
+#endif
   if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)

@@ -11,6 +11,10 @@ namespace nerf {
 
 struct SampleSrc;
 
+// Compute units of the current device (cached per device): the grid of the
+// persistent MLP kernels, one workgroup per CU.
+int current_device_cus();
+
 hipError_t launch_generate_rays(const float* c2w_rowmajor16, int width, int height, int row0, int row1,
                                 float focal, float* rays_o, float* rays_d, hipStream_t stream);
 hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSrc& src, long n_points,
