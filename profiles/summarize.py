@@ -1,13 +1,17 @@
 """Summarise a rocprofv3 collection (profiles/collect.sh) into per-kernel numbers.
 
-    python profiles/summarize.py gpurun_out/prof_r01 profiles/r01
+    python profiles/summarize.py gpurun_out/prof_<tag> profiles/<round>/<tag>
 
-Writes <dest>/summary.json and refreshes profiles/pmc_latest.json (read by
-bench.py for the roofline's ``traffic`` field).  HBM bytes per launch follow
+Writes <dest>/summary.json, copies the trace's kernel_stats.csv and the JSON line
+the profiled bench printed, and merges the MLP kernel's entry into
+profiles/pmc_latest.json (read by bench.py for the roofline's ``traffic`` field).
+
+The profiled command is the headline bench alone (collect.sh), so every MLP
+dispatch in it is a headline launch.  HBM bytes per launch follow
 MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced read, so it is
 doubled (the MLP kernel's reads are 16-B LDS-DMA weight pieces); WRITE_SIZE is
-exact for 16-B-per-lane stores.
+exact for 16-B-per-lane stores (the MLP's float4 (sigma, rgb) stores).
 """
 from __future__ import annotations
 
@@ -17,24 +21,15 @@ import os
 import shutil
 import sys
 
+HERE = os.path.dirname(os.path.abspath(__file__))
 
-def per_kernel(path, counter, by_grid=False):
+
+def per_kernel(path, counter):
     acc = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        key = (r["Kernel_Name"], int(r["Grid_Size"])) if by_grid else r["Kernel_Name"]
-        acc.setdefault(key, []).append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == counter:
+            acc.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
-
-
-def trace_by_grid(path):
-    """Mean duration per (kernel, grid size) from the kernel trace."""
-    acc = {}
-    for r in csv.DictReader(open(path)):
-        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-        acc.setdefault((r["Kernel_Name"], grid), []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-    return {k: (len(v), sum(v) / len(v)) for k, v in acc.items()}
 
 
 def main(src: str, dest: str) -> None:
@@ -42,35 +37,30 @@ def main(src: str, dest: str) -> None:
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                            "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6,
                             "pct": float(r["Percentage"])}
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     for k in stats:
         f, w = fetch.get(k), write.get(k)
         if f is not None and w is not None:
-            stats[k]["fetch_bytes_raw"] = f * 1024
-            stats[k]["write_bytes"] = w * 1024
+            stats[k]["fetch_size_kib"] = f
+            stats[k]["write_size_kib"] = w
             stats[k]["hbm_bytes_per_launch"] = 2 * f * 1024 + w * 1024
-    # per launch size (grid = threads): the same kernel runs several configurations
-    # (e.g. the bf16 MLP on 128-, 64- and 192-sample passes); bench.py picks the
-    # headline launch by its grid
-    fg = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE", True)
-    wg = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE", True)
-    tg = trace_by_grid(os.path.join(src, "trace", "run_kernel_trace.csv"))
-    for (name, grid), (calls, ms) in tg.items():
-        if name not in stats:
-            continue
-        e = {"calls": calls, "avg_ms": ms}
-        f, w = fg.get((name, grid)), wg.get((name, grid))
-        if f is not None and w is not None:
-            e.update({"fetch_bytes_raw": f * 1024, "write_bytes": w * 1024, "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024})
-        stats[name].setdefault("by_grid", {})[str(grid)] = e
-    out = {"source": src, "kernels": stats}
+    cmd = open(os.path.join(src, "command.txt")).read().strip()
+    bench = open(os.path.join(src, "bench_under_rocprof.json")).read().strip()
+    out = {"source": os.path.relpath(dest, os.path.dirname(HERE)), "command": "bench.py " + cmd,
+           "bench_under_rocprof": json.loads(bench.splitlines()[-1]), "kernels": stats}
     json.dump(out, open(os.path.join(dest, "summary.json"), "w"), indent=1)
-    shutil.copy(os.path.join(dest, "summary.json"), os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                                  "pmc_latest.json"))
-    for name in ("run_kernel_stats.csv",):
-        shutil.copy(os.path.join(src, "trace", name), os.path.join(dest, "kernel_stats.csv"))
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dest, "kernel_stats.csv"))
+    # merge the MLP kernels into pmc_latest.json (one entry per precision's kernel)
+    latest_p = os.path.join(HERE, "pmc_latest.json")
+    latest = json.load(open(latest_p)) if os.path.exists(latest_p) else {}
+    latest = {"kernels": latest.get("kernels", {}) if "by_grid" not in json.dumps(latest) else {}}
+    for k, v in stats.items():
+        if k.startswith("mlp_") and "hbm_bytes_per_launch" in v:
+            latest["kernels"][k] = dict(v, source=out["source"], command=out["command"])
+    json.dump(latest, open(latest_p, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
