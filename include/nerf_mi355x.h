@@ -165,6 +165,15 @@ int nerf_sample_points(nerf_ctx* ctx, const float* rays_o, const float* rays_d, 
 int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable);
 int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out /* [NERF_N_STAGES] */);
 
+/* Context options (no reference counterpart: implementation switches of this library).
+ *   NERF_OPT_FUSED_COMPOSITE (default 1): in nerf_render / nerf_render_sampled, bf16 and
+ *   fp8 passes whose per-ray sample count is a multiple of 32 composite inside the MLP
+ *   kernel (per-32-sample partial integrals, chained per ray; the same sums as
+ *   execute_volume_rendering, src/benchmark/pytorch_renderers.py:105-125, regrouped).
+ *   0 writes (sigma, rgb) per sample and runs the sequential composite kernel. */
+#define NERF_OPT_FUSED_COMPOSITE 1
+int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,7 @@ struct nerf_ctx {
   size_t w_cap = 0;            // floats
   float* host_stage = nullptr; // pinned: z table + u
   bool profiling = false;
+  bool fused_composite = true; // NERF_OPT_FUSED_COMPOSITE
   hipEvent_t ev[NERF_N_STAGES + 1] = {};
   bool stage_ran[NERF_N_STAGES] = {};
 };
@@ -104,10 +105,10 @@ struct DeviceGuard {
 };
 
 hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, long n, float* out, bool expl,
-                   hipStream_t s) {
+                   hipStream_t s, float* seg = nullptr) {
   const NetDev& nd = ctx->net[net];
-  if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s);
-  if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s);
+  if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg);
+  if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
 }
 
@@ -274,6 +275,15 @@ int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable) {
   return NERF_OK;
 }
 
+int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value) {
+  if (!ctx) return set_error(NERF_E_INVALID, "null context");
+  if (option == NERF_OPT_FUSED_COMPOSITE) {
+    ctx->fused_composite = value != 0;
+    return NERF_OK;
+  }
+  return set_error(NERF_E_INVALID, "unknown option %d", option);
+}
+
 int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out) {
   if (!ctx || !ms_out) return set_error(NERF_E_INVALID, "null argument");
   DeviceGuard g(ctx->device);
@@ -376,14 +386,22 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
     if ((rc = mark(2)) != NERF_OK) return rc;
   }
   if ((rc = mark(3)) != NERF_OK) return rc;
+  // bf16 / fp8 with whole 32-sample segments per ray: compositing fused into the
+  // MLP epilogue (one record per segment), then chained per ray; the fp32 parity
+  // path keeps the sequential composite kernel
+  const bool fused = ctx->fused_composite && precision != NERF_FP32 && n_fine > 1 && n_fine % 32 == 0;
   {
     SampleSrc src{rays_o, rays_d, z_main, z_stride, n_fine, nullptr, nullptr};
-    HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s));
+    HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s,
+                    fused ? ctx->mlp_out : nullptr));
     ctx->stage_ran[3] = true;
   }
   if ((rc = mark(4)) != NERF_OK) return rc;
-  HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_main, z_stride, rays_d, int(n_rays), n_fine,
-                           rgb_out, depth_out, nullptr, nullptr, s));
+  if (fused)
+    HIP_TRY(launch_composite_segments(ctx->mlp_out, int(n_rays), n_fine / 32, rgb_out, depth_out, s));
+  else
+    HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_main, z_stride, rays_d, int(n_rays), n_fine,
+                             rgb_out, depth_out, nullptr, nullptr, s));
   ctx->stage_ran[4] = true;
   HIP_TRY(hipEventRecord(ctx->ev[NERF_N_STAGES], s));
   return NERF_OK;

@@ -81,7 +81,8 @@ static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile
 static_assert(kTotalChunks * kChunkB <= kBf16BlobBytes, "device blob is padded for every chunk geometry");
 constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kCols * 4 * 1024;
-constexpr int kLdsStampOff = kLdsDeOff + kWaves * kCols * 2 * 1024;
+constexpr int kLdsSegOff = kLdsDeOff + kWaves * kCols * 2 * 1024;       // fused compositing: (dist, z) per sample
+constexpr int kLdsStampOff = kLdsSegOff + kWaves * kCols * kSamplesPerWave * 8;
 #ifdef NERF_STAMPS
 constexpr int kLdsBytes = kLdsStampOff + kWaves * (2 + 3 * kTotalChunks + 1) * 8;
 #else
@@ -394,21 +395,29 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
   }
 }
 
-// (sigma, r, g, b) of a tile's samples; p0 < 0: nothing pending
-__device__ __forceinline__ void store_results(const f32x4 (&res)[kCols], long p0, long n_points, int h,
-                                              f32x4* __restrict__ out) {
+// (sigma, r, g, b) of a tile's samples, or with fused compositing (seg) each
+// column's segment record (nerf_device.h SegRecord, lanes 0 and 1); p0 < 0:
+// nothing pending
+__device__ __forceinline__ void store_results(const f32x4 (&res)[kCols], long p0, long n_points, int lane,
+                                              f32x4* __restrict__ out, f32x4* __restrict__ seg) {
   if (p0 < 0) return;
 #pragma unroll
   for (int c = 0; c < kCols; ++c) {
     const long p = p0 + c * kSamplesPerWave;
-    if (p < n_points && h == 0) out[p] = res[c];
+    if (seg) {
+      const long first = p - (lane & 31);                 // the segment's first sample
+      if (first < n_points && lane < 2) seg[(first / kSamplesPerWave) * 2 + lane] = res[c];
+    } else if (p < n_points && lane < 32) {
+      out[p] = res[c];
+    }
   }
 }
 
 template <bool kExplicit>
 __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __restrict__ blob,
                                                                const float* __restrict__ prm_g, SampleSrc src,
-                                                               long n_points, f32x4* __restrict__ out) {
+                                                               long n_points, f32x4* __restrict__ out,
+                                                               f32x4* __restrict__ seg) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -452,7 +461,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     for (int c = 0; c < kCols; ++c) {
       const long p = p0 + c * kSamplesPerWave;
       float x[3], d[3], pef[32], def[16];
-      fetch_sample<kExplicit>(src, p < n_points ? p : n_points - 1, x, d);
+      float dist = 0.0f, zz = 0.0f;
+      if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
+      else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, seg != nullptr, x, d, dist, zz);
 #if defined(NERF_ABLATE_ENCODING) || defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no sin/cos
 #pragma unroll
       for (int q = 0; q < 32; ++q) pef[q] = x[q % 3] * float(q);
@@ -468,6 +479,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       for (int u = 0; u < 4; ++u) *(bf16x8*)(pe_dst + u * 1024) = pack8(pef + 8 * u);
       *(bf16x8*)(de_dst) = pack8(def);
       *(bf16x8*)(de_dst + 1024) = pack8(def + 8);
+      if (!kExplicit && seg != nullptr) {   // the integral's network-independent inputs (nerf_device.h)
+        if (h == 0) *(f32x2_t*)(lds + kLdsSegOff + ((wave_u * kCols + c) * kSamplesPerWave + (lane & 31)) * 8) = f32x2_t{dist, zz};
+      }
     }
 
     // Seam E_-1: chunk 0 landed (own pieces) and is published, parameters too
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     __syncthreads();
     stage_chunk(cx.blob, kSlots - 2, lds, wave_u, lane);
     NERF_STAMP(cx, 1);
-    store_results(res, res_p0, n_points, h, out);
+    store_results(res, res_p0, n_points, lane, out, seg);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
     f32x16 acc[kCols][8];
 #pragma unroll
@@ -539,8 +553,13 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
           for (int c = 0; c < kCols; ++c) convert_dword(acc[c][2 + (m >> 3)], m & 7, bA[c][2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
     }
 #pragma unroll
-    for (int c = 0; c < kCols; ++c)
+    for (int c = 0; c < kCols; ++c) {
       res[c] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
+      if (!kExplicit && seg != nullptr) {
+        const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + ((wave_u * kCols + c) * kSamplesPerWave + (lane & 31)) * 8);
+        res[c] = seg_composite(res[c], in[0], in[1], lane);
+      }
+    }
     res_p0 = p0;
 #ifdef NERF_STAMPS
     NERF_STAMP(cx, kStampSlots - 1);
@@ -556,7 +575,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
         g_nerf_stamps[tile - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
 #endif
   }
-  store_results(res, res_p0, n_points, h, out);
+  store_results(res, res_p0, n_points, lane, out, seg);
   // the stream ran kSlots-2 chunks into a tile that does not exist: let them
   // land before the workgroup's LDS is released
   wait_vmcnt(0);
@@ -565,7 +584,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 }  // namespace
 
 hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                           bool explicit_points, hipStream_t stream) {
+                           bool explicit_points, hipStream_t stream, float* seg) {
   if (n_points <= 0) return hipSuccess;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 #ifdef NERF_BF16_ONE_TILE
@@ -577,10 +596,10 @@ hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSr
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)
     hipLaunchKernelGGL(mlp_bf16_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out);
+                       (f32x4*)out, (f32x4*)seg);
   else
     hipLaunchKernelGGL(mlp_bf16_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out);
+                       (f32x4*)out, (f32x4*)seg);
   return hipGetLastError();
 }
 

@@ -60,7 +60,8 @@ constexpr int kLdsParamOff = kSlots * kChunkB;
 constexpr int kLdsScaleOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
 constexpr int kLdsPeOff = kLdsScaleOff + kFp8ScaleBytes;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * 2048;
-constexpr int kLdsBytes = kLdsDeOff + kWaves * 2048;
+constexpr int kLdsSegOff = kLdsDeOff + kWaves * 2048;                 // fused compositing: (dist, z) per sample
+constexpr int kLdsBytes = kLdsSegOff + kWaves * kSamplesPerWave * 8;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 constexpr int kDeFromPe = kLdsDeOff - kLdsPeOff;                      // one address VGPR for both encodings
 static_assert(kDeFromPe + 1024 + 16 <= 65536, "direction reads fit the ds_read offset field");
@@ -308,7 +309,8 @@ __device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x
 template <bool kExplicit>
 __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __restrict__ blob,
                                                               const float* __restrict__ prm_g, SampleSrc src,
-                                                              long n_points, f32x4* __restrict__ out) {
+                                                              long n_points, f32x4* __restrict__ out,
+                                                              f32x4* __restrict__ seg) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -329,7 +331,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     ((f32x4*)(lds + kLdsScaleOff))[i] = ((const f32x4*)(blob + kFp8ScaleOff))[i];
   {
     float x[3], d[3], pef[32], def[16];
-    fetch_sample<kExplicit>(src, p < n_points ? p : n_points - 1, x, d);
+    float dist = 0.0f, zz = 0.0f;
+    if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
+    else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, seg != nullptr, x, d, dist, zz);
     pos_encode<true>(x[0], x[1], x[2], h, pef);
     dir_encode<true>(d[0], d[1], d[2], h, def);
     // raw coordinates (slots 30, 31 of half 0, slot 30 of half 1) clamped to the e4m3 range
@@ -349,6 +353,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     for (int i = 0; i < 4; ++i) w0[i] = cvt4(def[4 * i], def[4 * i + 1], def[4 * i + 2], def[4 * i + 3]);
     de_dst[0] = w0;
     de_dst[64] = i32x4{0, 0, 0, 0};                    // direction slots 16..31: padding
+    if (!kExplicit && seg != nullptr) {                // the integral's network-independent inputs
+      if (h == 0) *(f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane & 31)) * 8) = f32x2_t{dist, zz};
+    }
   }
   wait_vmcnt(kGldsPerStage * (kSlots - 2));            // chunk 0 landed (own pieces)
   __syncthreads();
@@ -413,23 +420,31 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   // reload a vmcnt(0) drain of the weight stream
   const int lane_o = int(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
   const long p_o = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane_o & 31);
-  if (p_o < n_points && h == 0) out[p_o] = f32x4{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
+  const f32x4 res{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
+  if (!kExplicit && seg != nullptr) {                  // fused compositing: one record per segment
+    const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane_o & 31)) * 8);
+    const f32x4 rec = seg_composite(res, in[0], in[1], lane_o);
+    const long first = p_o - (lane_o & 31);
+    if (first < n_points && lane_o < 2) seg[(first / kSamplesPerWave) * 2 + lane_o] = rec;
+  } else if (p_o < n_points && h == 0) {
+    out[p_o] = res;
+  }
 }
 
 }  // namespace
 
 hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                          bool explicit_points, hipStream_t stream) {
+                          bool explicit_points, hipStream_t stream, float* seg) {
   if (n_points <= 0) return hipSuccess;
   const long blocks = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)
     hipLaunchKernelGGL(mlp_fp8_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out);
+                       (f32x4*)out, (f32x4*)seg);
   else
     hipLaunchKernelGGL(mlp_fp8_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out);
+                       (f32x4*)out, (f32x4*)seg);
   return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@ namespace nerf {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 // fl32(2^k * pi): `freq * torch.pi` with freq = 2.0**k as fp32 (nerf.py:22,42);
 // a power-of-two multiple of fl32(pi), so exact.
@@ -233,6 +234,103 @@ __device__ __forceinline__ void fetch_sample(const SampleSrc& src, long p, float
       x[c] = sample_coord(src.rays_o[3 * ray + c], d[c], zz);
     }
   }
+}
+
+// ---- Compositing fused into the MLP epilogue (bf16 / fp8 render passes) ----
+// The volume integral of execute_volume_rendering (pytorch_renderers.py:105-125)
+// is associative over consecutive samples of a ray.  With S % 32 == 0 a wave's
+// 32-sample column tile is one "segment" of one ray, so each wave composites
+// its own segment in registers, and only a 32-B record per segment leaves the
+// kernel (instead of 16 B per sample):
+//   P      = prod_i (1 - alpha_i + 1e-10)            (double)
+//   rgb, d = sum_i alpha_i * float(P_<i) * (c_i, z_i)  (fp32, P_<i the in-segment
+//                                                        exclusive product)
+// and composite_segments_kernel chains the records of a ray:
+//   out = sum_k float(T_k) * part_k,  T_{k+1} = T_k * P_k  (double),
+// which is the reference's sequential sum regrouped (differences at fp32
+// rounding level; the fp32 parity path keeps the sequential kernel).
+struct SegRecord {      // 32 B; written as two f32x4 by lanes 0 and 1 of the segment
+  double P;
+  float r, g, b, depth, acc, pad;
+};
+static_assert(sizeof(SegRecord) == 32, "segment record is two 16-B stores");
+
+// Sample point, view direction and -- for fused compositing (seg) -- the
+// integral's network-independent inputs of render-pass sample p:
+// dist = (z_{s+1} - z_s, or 1e10 for the ray's last sample) * |d| and z_s, in the
+// reference's operation order (pytorch_renderers.py:106-112).  idx32 (wave-
+// uniform: the launch has fewer than 2^32 samples) divides in 32 bits.
+__device__ __forceinline__ void fetch_render_sample(const SampleSrc& src, long p, bool idx32, bool seg,
+                                                    float (&x)[3], float (&d)[3], float& dist, float& z) {
+  const long ray = idx32 ? long(unsigned(p) / unsigned(src.n_samples)) : p / src.n_samples;
+  const int s = int(p - ray * src.n_samples);
+  const float* zr = src.z + ray * src.z_stride;
+  z = zr[s];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    d[c] = src.rays_d[3 * ray + c];
+    x[c] = sample_coord(src.rays_o[3 * ray + c], d[c], z);
+  }
+  if (seg) {
+    const float norm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d[0], d[0]), __fmul_rn(d[1], d[1])), __fmul_rn(d[2], d[2])));
+    const float delta = s + 1 < src.n_samples ? __fsub_rn(zr[s + 1], z) : 1e10f;
+    dist = __fmul_rn(delta, norm);
+  }
+}
+
+// DPP moves within 32-lane segments (gfx9 encodings): row_shr:n = 0x110+n,
+// row_bcast:15 = 0x142 (rows 1 and 3 take lane 15 of the row below: row_mask
+// 0xa), wave_shr:1 = 0x138.  Lanes without a source keep `identity`.
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ float dpp_f32(float v, float identity) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, identity),
+                                                               __builtin_bit_cast(int, v), kCtrl, kRowMask, 0xf, false));
+}
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ double dpp_f64(double v, double identity) {
+  typedef int i32x2_t __attribute__((ext_vector_type(2)));
+  const i32x2_t vi = __builtin_bit_cast(i32x2_t, v), oi = __builtin_bit_cast(i32x2_t, identity);
+  const i32x2_t r{__builtin_amdgcn_update_dpp(oi[0], vi[0], kCtrl, kRowMask, 0xf, false),
+                  __builtin_amdgcn_update_dpp(oi[1], vi[1], kCtrl, kRowMask, 0xf, false)};
+  return __builtin_bit_cast(double, r);
+}
+// inclusive scans over each 32-lane segment (Hillis-Steele within 16-lane rows,
+// then row 1 (3) folds in lane 15 (47))
+__device__ __forceinline__ double seg_scan_mul(double v) {
+  v = __dmul_rn(dpp_f64<0x111>(v, 1.0), v);
+  v = __dmul_rn(dpp_f64<0x112>(v, 1.0), v);
+  v = __dmul_rn(dpp_f64<0x114>(v, 1.0), v);
+  v = __dmul_rn(dpp_f64<0x118>(v, 1.0), v);
+  return __dmul_rn(dpp_f64<0x142, 0xa>(v, 1.0), v);
+}
+__device__ __forceinline__ float seg_scan_add(float v) {
+  v = __fadd_rn(dpp_f32<0x111>(v, 0.0f), v);
+  v = __fadd_rn(dpp_f32<0x112>(v, 0.0f), v);
+  v = __fadd_rn(dpp_f32<0x114>(v, 0.0f), v);
+  v = __fadd_rn(dpp_f32<0x118>(v, 0.0f), v);
+  return __fadd_rn(dpp_f32<0x142, 0xa>(v, 0.0f), v);
+}
+__device__ __forceinline__ float lane31(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 31));
+}
+
+// Composite the segment held by lanes 0..31 (sample j of the segment in lane j;
+// lanes 32..63 scan their own copy, which no caller stores).  v = (sigma, r, g, b).
+// Returns this lane's 16 B of the record (even lanes: P, r, g; odd: b, depth, acc, 0).
+__device__ __forceinline__ f32x4 seg_composite(f32x4 v, float dist, float z, int lane) {
+  const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-relu(v[0]), dist)));
+  const double P = seg_scan_mul(double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
+  const double Pex = dpp_f64<0x138>(P, 1.0);                   // exclusive: lane j takes lane j-1, lane 0 1.0
+  const float w = __fmul_rn(alpha, float(Pex));
+  const float r = lane31(seg_scan_add(__fmul_rn(w, v[1])));
+  const float g = lane31(seg_scan_add(__fmul_rn(w, v[2])));
+  const float b = lane31(seg_scan_add(__fmul_rn(w, v[3])));
+  const float dep = lane31(seg_scan_add(__fmul_rn(w, z)));
+  const float acc = lane31(seg_scan_add(w));
+  const f32x2_t Pseg = __builtin_bit_cast(f32x2_t, P);
+  const f32x4 lo{lane31(Pseg[0]), lane31(Pseg[1]), r, g};
+  const f32x4 hi{b, dep, acc, 0.0f};
+  return (lane & 1) ? hi : lo;
 }
 
 }  // namespace nerf

@@ -19,10 +19,15 @@ hipError_t launch_generate_rays(const float* c2w_rowmajor16, int width, int heig
                                 float focal, float* rays_o, float* rays_d, hipStream_t stream);
 hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSrc& src, long n_points,
                           float* out, bool explicit_points, hipStream_t stream);
+// seg (render passes with n_samples % 32 == 0 only): compositing fused into the
+// epilogue, one 32-B SegRecord per 32-sample segment instead of out's (sigma, rgb)
 hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points,
-                           float* out, bool explicit_points, hipStream_t stream);
+                           float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr);
 hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points,
-                          float* out, bool explicit_points, hipStream_t stream);
+                          float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr);
+// Chains each ray's segment records into (rgb, depth) (nerf_device.h SegRecord).
+hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
+                                     hipStream_t stream);
 hipError_t launch_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride,
                             const float* z, int z_ray_stride, const float* rays_d, int n_rays, int n_samples,
                             float* rgb_out, float* depth_out, float* acc_out, float* weights_out,

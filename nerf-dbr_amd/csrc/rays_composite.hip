@@ -277,6 +277,32 @@ __global__ void composite_packed_kernel(const f32x4* __restrict__ mlp, const flo
   if (acc_out) acc_out[r] = acc;
 }
 
+// Second half of the compositing fused into the bf16 / fp8 MLP epilogue
+// (nerf_device.h SegRecord): chain a ray's segment records in order,
+//   rgb += float(T) * rgb_k, depth += float(T) * depth_k, T *= P_k (double),
+// the regrouped form of composite_kernel's sequential sums.  One thread per ray.
+__global__ void composite_segments_kernel(const SegRecord* __restrict__ seg, int n_rays, int n_segments,
+                                          float* __restrict__ rgb_out, float* __restrict__ depth_out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const SegRecord* sr = seg + long(r) * n_segments;
+  double T = 1.0;
+  float cr = 0.0f, cg = 0.0f, cb = 0.0f, dep = 0.0f;
+  for (int k = 0; k < n_segments; ++k) {
+    const SegRecord rec = sr[k];
+    const float t = float(T);
+    cr = __fadd_rn(cr, __fmul_rn(t, rec.r));
+    cg = __fadd_rn(cg, __fmul_rn(t, rec.g));
+    cb = __fadd_rn(cb, __fmul_rn(t, rec.b));
+    dep = __fadd_rn(dep, __fmul_rn(t, rec.depth));
+    T = __dmul_rn(T, rec.P);
+  }
+  rgb_out[3L * r] = cr;
+  rgb_out[3L * r + 1] = cg;
+  rgb_out[3L * r + 2] = cb;
+  depth_out[r] = dep;
+}
+
 // Sample depths and points, one thread per (ray, sample).
 // Uniform (BaseUnifiedRenderer.sample_points_on_rays, base_renderer.py:260-281):
 //   z = table[s] (near*(1-t)+far*t, built on the host bit-exactly).
@@ -349,6 +375,16 @@ hipError_t launch_composite(const float* sigma, int sigma_stride, const float* r
   }
   hipLaunchKernelGGL(composite_kernel, grid, block, 0, stream, sigma, sigma_stride, rgb, rgb_stride, z, z_ray_stride,
                      rays_d, n_rays, n_samples, rgb_out, depth_out, acc_out, weights_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
+                                     hipStream_t stream) {
+  if (n_rays <= 0) return hipSuccess;
+  const int threads = 256;
+  const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  hipLaunchKernelGGL(composite_segments_kernel, grid, block, 0, stream, (const SegRecord*)seg, n_rays, n_segments,
+                     rgb_out, depth_out);
   return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ NERF_FP32, NERF_BF16, NERF_FP8 = 0, 1, 2
 NERF_NET_COARSE, NERF_NET_FINE = 0, 1
 NERF_N_PARAMS = 22
 NERF_N_STAGES = 5
+NERF_OPT_FUSED_COMPOSITE = 1
 STAGES = ("rays", "coarse_mlp", "importance", "fine_mlp", "composite")
 
 PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16, "fp8": NERF_FP8}
@@ -63,6 +64,7 @@ SIGNATURES = {
                                       _P]),
     "nerf_ctx_set_profiling": (_c.c_int, [_P, _c.c_int]),
     "nerf_ctx_stage_ms": (_c.c_int, [_P, _FP]),
+    "nerf_ctx_set_option": (_c.c_int, [_P, _c.c_int, _c.c_int]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -264,6 +266,10 @@ class Device:
 
     def set_profiling(self, enable: bool) -> None:
         _check(self.lib.nerf_ctx_set_profiling(self._ctx, 1 if enable else 0))
+
+    def set_fused_composite(self, enable: bool) -> None:
+        """NERF_OPT_FUSED_COMPOSITE: compositing in the bf16/fp8 MLP epilogue (default on)."""
+        _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_FUSED_COMPOSITE, 1 if enable else 0))
 
     def stage_ms(self) -> dict:
         ms = (ctypes.c_float * NERF_N_STAGES)()

@@ -436,3 +436,41 @@ def test_multi_rank_rehearsal_on_one_device():
     assert len(lines) == 1, res.stdout
     b = js.loads(lines[0])
     assert b["n_gpus"] == 2 and b["value"] > 0 and b["config"]["parallelism"].startswith("row-band x2")
+
+
+# ------------------------------------- compositing fused into the MLP epilogue --
+@pytest.mark.parametrize("precision,spp,n_imp", [("bf16", 32, 0), ("bf16", 128, 0), ("bf16", 64, 128),
+                                                 ("fp8", 128, 0), ("fp8", 64, 128), ("bf16", 48, 0)])
+def test_fused_composite_matches_sequential(ckpt, precision, spp, n_imp):
+    """NERF_OPT_FUSED_COMPOSITE: per-32-sample partial integrals chained per ray are
+    the sequential composite regrouped, on the same network outputs (fp32 rounding
+    level; 1e-5 written here).  spp=48 (not a multiple of 32) keeps the sequential
+    kernel, so it must agree bit for bit."""
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    r = MI355XRenderer(precision, n_importance=n_imp)
+    r.setup(ckpt)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
+    res = (67, 41)                                  # ragged: the last MLP tile is partial
+    r.hip.set_fused_composite(False)
+    rgb_s, d_s = r.render_image(pose, res, spp)
+    r.hip.set_fused_composite(True)
+    rgb_f, d_f = r.render_image(pose, res, spp)
+    er, ed = maxabs(rgb_f, rgb_s.cpu().numpy()), maxabs(d_f, d_s.cpu().numpy())
+    print(f"fused vs sequential composite {precision} {spp}+{n_imp}: rgb {er:.2e} depth {ed:.2e}")
+    if (spp + n_imp) % 32:
+        assert er == 0.0 and ed == 0.0
+    else:
+        assert er < 1e-5 and ed < 1e-5 * 6.0
+
+
+def test_fused_composite_headline_vs_fp32(r16, r32):
+    """The benchmark configuration with the fused epilogue stays within the bf16
+    error band against the fp32 parity path (which is < 1e-4 vs the reference)."""
+    pose = torch.eye(4)
+    pose[2, 3] = 4.0
+    rgb16, d16 = r16.render_rows(pose, (800, 600), 128, 292, 308)
+    rgb32, d32 = r32.render_rows(pose, (800, 600), 128, 292, 308)
+    er, ed = maxabs(rgb16, rgb32.cpu().numpy()), maxabs(d16, d32.cpu().numpy())
+    print(f"bf16 fused vs fp32, 800x600x128 rows 292-308: rgb {er:.2e} depth {ed:.2e}")
+    assert er < 5e-3 and ed < 2e-2

@@ -26,18 +26,23 @@ from nerf_amd import weights as W  # noqa: E402
 
 
 class Lib:
-    def __init__(self, path: str, sd_fine, precision: int):
-        self.path = path
+    def __init__(self, spec: str, sd_fine, precision: int):
+        # spec: path[:nofuse] -- ':nofuse' turns NERF_OPT_FUSED_COMPOSITE off
+        self.path = spec
+        path, _, opt = spec.partition(":")
         self.lib = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
         for name, (res, args) in rt.SIGNATURES.items():
-            fn = getattr(self.lib, name)
-            fn.restype, fn.argtypes = res, args
+            fn = getattr(self.lib, name, None)          # older builds lack newer entry points
+            if fn is not None:
+                fn.restype, fn.argtypes = res, args
         self.ctx = ctypes.c_void_p()
         assert self.lib.nerf_ctx_create(0, ctypes.byref(self.ctx)) == 0, self.err()
         keep, ptrs = rt._param_list(sd_fine)
         for net in (0, 1):
             assert self.lib.nerf_ctx_load_weights(self.ctx, net, ptrs, rt.NERF_N_PARAMS) == 0, self.err()
         self.lib.nerf_ctx_set_profiling(self.ctx, 1)
+        if opt == "nofuse":
+            assert self.lib.nerf_ctx_set_option(self.ctx, rt.NERF_OPT_FUSED_COMPOSITE, 0) == 0, self.err()
         self.precision = precision
 
     def err(self):
@@ -51,7 +56,7 @@ class Lib:
         assert rc == 0, self.err()
         ms = (ctypes.c_float * rt.NERF_N_STAGES)()
         assert self.lib.nerf_ctx_stage_ms(self.ctx, ms) == 0, self.err()
-        return ms[3]
+        return ms[3], ms[4]
 
 
 def main():
@@ -80,14 +85,18 @@ def main():
         if ref is None:
             ref = img
         diffs[lib.path] = float((img - ref).abs().max())
+    comp = {lib.path: [] for lib in libs}
     for _ in range(args.rounds):
         for lib in libs:
-            times[lib.path].append(lib.render(pose, t, rgb, depth))
+            mlp_ms, comp_ms = lib.render(pose, t, rgb, depth)
+            times[lib.path].append(mlp_ms)
+            comp[lib.path].append(comp_ms)
     flop = 800 * 600 * args.spp * W.FLOPS_PER_SAMPLE
     out = {}
     for p, v in times.items():
         med = float(np.median(v))
         out[os.path.basename(p)] = {"median_ms": med, "min_ms": float(np.min(v)),
+                                    "composite_median_ms": float(np.median(comp[p])),
                                     "tflops": flop / med / 1e9, "max_abs_vs_first": diffs[p]}
     print(json.dumps(out, indent=1))
 
