@@ -164,6 +164,9 @@ int nerf_sample_points(nerf_ctx* ctx, const float* rays_o, const float* rays_d, 
 #define NERF_N_STAGES 5
 int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable);
 int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out /* [NERF_N_STAGES] */);
+/* The same for each of the last n renders (n <= 64, oldest first), so that a run of
+ * back-to-back renders can be timed per stage without a host synchronisation per frame. */
+int nerf_ctx_stage_ms_history(nerf_ctx* ctx, int n, float* ms_out /* [n][NERF_N_STAGES] */);
 
 /* Context options (no reference counterpart: implementation switches of this library).
  *   NERF_OPT_FUSED_COMPOSITE (default 1): in nerf_render / nerf_render_sampled, bf16 and

@@ -63,10 +63,24 @@ struct nerf_ctx {
   float* wbuf = nullptr;       // coarse weights [R][S] + u [N]
   size_t w_cap = 0;            // floats
   float* host_stage = nullptr; // pinned: z table + u
+  // what the last upload put on the device (nerf_render skips an unchanged upload,
+  // so back-to-back renders queue without a host synchronisation)
+  std::vector<float> up_z, up_u;
+  const float* up_zbuf = nullptr;
+  const float* up_wbuf = nullptr;
+  hipEvent_t stage_ev = nullptr; // recorded after the last upload from host_stage
   bool profiling = false;
   bool fused_composite = true; // NERF_OPT_FUSED_COMPOSITE
-  hipEvent_t ev[NERF_N_STAGES + 1] = {};
-  bool stage_ran[NERF_N_STAGES] = {};
+  // stage events of the last kEvFrames renders (a ring, so that per-frame stage
+  // times can be read after a run of back-to-back renders without a host sync each)
+  struct Frame {
+    hipEvent_t ev[NERF_N_STAGES + 1] = {};
+    bool ran[NERF_N_STAGES] = {};
+    bool profiled = false;
+  };
+  static constexpr int kEvFrames = 64;
+  Frame frames[kEvFrames];
+  long n_frames = 0;              // renders issued on this context
 };
 
 namespace {
@@ -141,7 +155,9 @@ int nerf_ctx_create(int device, nerf_ctx** out) {
   DeviceGuard g(device);
   nerf_ctx* ctx = new nerf_ctx();
   ctx->device = device;
-  for (auto& e : ctx->ev) HIP_TRY(hipEventCreate(&e));
+  for (auto& f : ctx->frames)
+    for (auto& e : f.ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventCreateWithFlags(&ctx->stage_ev, hipEventDisableTiming));
   HIP_TRY(hipHostMalloc((void**)&ctx->host_stage, sizeof(float) * 2048, hipHostMallocDefault));
   *out = ctx;
   return NERF_OK;
@@ -160,8 +176,10 @@ void nerf_ctx_destroy(nerf_ctx* ctx) {
   for (float* p : {ctx->rays, ctx->mlp_out, ctx->zbuf, ctx->wbuf})
     if (p) (void)hipFree(p);
   if (ctx->host_stage) (void)hipHostFree(ctx->host_stage);
-  for (auto& e : ctx->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& f : ctx->frames)
+    for (auto& e : f.ev)
+      if (e) (void)hipEventDestroy(e);
+  if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
   delete ctx;
 }
 
@@ -263,6 +281,8 @@ int nerf_sample_points(nerf_ctx* ctx, const float* rays_o, const float* rays_d, 
   int rc = grow(ctx->zbuf, ctx->z_cap, 1024, "z");
   if (rc != NERF_OK) return rc;
   HIP_TRY(hipStreamSynchronize(s));   // host_stage may still feed a previous copy
+  HIP_TRY(hipEventSynchronize(ctx->stage_ev));
+  ctx->up_zbuf = nullptr;             // the table slot is overwritten below
   nerf_uniform_z(t_vals, n_samples, near_, far_, ctx->host_stage);
   HIP_TRY(hipMemcpyAsync(ctx->zbuf, ctx->host_stage, sizeof(float) * n_samples, hipMemcpyHostToDevice, s));
   HIP_TRY(launch_sample(ctx->zbuf, t_rand, n_rays, n_samples, rays_o, rays_d, z_out, points_out, s));
@@ -284,15 +304,31 @@ int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value) {
   return set_error(NERF_E_INVALID, "unknown option %d", option);
 }
 
-int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out) {
+int nerf_ctx_stage_ms_history(nerf_ctx* ctx, int n, float* ms_out) {
   if (!ctx || !ms_out) return set_error(NERF_E_INVALID, "null argument");
+  if (n <= 0 || n > nerf_ctx::kEvFrames || n > ctx->n_frames)
+    return set_error(NERF_E_INVALID, "stage history of %d frames: %ld rendered, ring of %d", n, ctx->n_frames,
+                     nerf_ctx::kEvFrames);
   DeviceGuard g(ctx->device);
-  HIP_TRY(hipEventSynchronize(ctx->ev[NERF_N_STAGES]));
-  for (int i = 0; i < NERF_N_STAGES; ++i) {
-    ms_out[i] = 0.0f;
-    if (ctx->profiling && ctx->stage_ran[i]) HIP_TRY(hipEventElapsedTime(&ms_out[i], ctx->ev[i], ctx->ev[i + 1]));
+  for (int k = 0; k < n; ++k) {
+    const nerf_ctx::Frame& f = ctx->frames[(ctx->n_frames - n + k) % nerf_ctx::kEvFrames];
+    HIP_TRY(hipEventSynchronize(f.ev[NERF_N_STAGES]));
+    for (int i = 0; i < NERF_N_STAGES; ++i) {
+      float* o = ms_out + k * NERF_N_STAGES + i;
+      *o = 0.0f;
+      if (f.profiled && f.ran[i]) HIP_TRY(hipEventElapsedTime(o, f.ev[i], f.ev[i + 1]));
+    }
   }
   return NERF_OK;
+}
+
+int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out) {
+  if (!ctx || !ms_out) return set_error(NERF_E_INVALID, "null argument");
+  if (ctx->n_frames == 0) {
+    for (int i = 0; i < NERF_N_STAGES; ++i) ms_out[i] = 0.0f;
+    return NERF_OK;
+  }
+  return nerf_ctx_stage_ms_history(ctx, 1, ms_out);
 }
 
 int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal, float near_,
@@ -323,11 +359,9 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
 
-  // z table (base_renderer.py:274-275) and the importance draw, via pinned staging
-  HIP_TRY(hipStreamSynchronize(s));   // host_stage may still feed a previous copy
-  float* hz = ctx->host_stage;
-  nerf_uniform_z(t_vals, n_samples, near_, far_, hz);
-  float* hu = hz + 1024;
+  // z table (base_renderer.py:274-275) and the importance draw
+  std::vector<float> hz(n_samples), hu(n_importance);
+  nerf_uniform_z(t_vals, n_samples, near_, far_, hz.data());
   for (int k = 0; k < n_importance; ++k)
     hu[k] = u ? u[k] : (n_importance > 1 ? float(k) / float(n_importance - 1) : 0.0f);
 
@@ -336,9 +370,12 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   // z buffer: [table 1024][stratified first-pass z, R x S][fine z, R x (S+N)]
   const size_t strat_floats = t_rand ? size_t(n_rays) * n_samples : 0;
   const size_t zfloats = 1024 + strat_floats + (n_importance > 0 ? size_t(n_rays) * n_fine : 0);
+  const size_t z_cap0 = ctx->z_cap, w_cap0 = ctx->w_cap;
   if ((rc = grow(ctx->zbuf, ctx->z_cap, zfloats, "z")) != NERF_OK) return rc;
   const size_t wfloats = 1024 + (n_importance > 0 ? size_t(n_rays) * n_samples : 0);
   if ((rc = grow(ctx->wbuf, ctx->w_cap, wfloats, "weights")) != NERF_OK) return rc;
+  if (ctx->z_cap != z_cap0) ctx->up_zbuf = nullptr;   // reallocated: the uploaded tables are gone
+  if (ctx->w_cap != w_cap0) ctx->up_wbuf = nullptr;
 
   float* d_ztab = ctx->zbuf;
   float* d_zstrat = ctx->zbuf + 1024;
@@ -347,12 +384,31 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   float* d_w = ctx->wbuf + 1024;
   float* rays_o = ctx->rays;
   float* rays_d = ctx->rays + n_rays * 3;
-  HIP_TRY(hipMemcpyAsync(d_ztab, hz, sizeof(float) * n_samples, hipMemcpyHostToDevice, s));
-  if (n_importance > 0) HIP_TRY(hipMemcpyAsync(d_u, hu, sizeof(float) * n_importance, hipMemcpyHostToDevice, s));
+  // upload through pinned staging only what changed since the last render
+  const bool need_z = !(ctx->up_zbuf == ctx->zbuf && ctx->up_z == hz);
+  const bool need_u = n_importance > 0 && !(ctx->up_wbuf == ctx->wbuf && ctx->up_u == hu);
+  if (need_z || need_u) {
+    HIP_TRY(hipEventSynchronize(ctx->stage_ev));   // host_stage no longer feeds an earlier copy
+    if (need_z) {
+      std::memcpy(ctx->host_stage, hz.data(), sizeof(float) * n_samples);
+      HIP_TRY(hipMemcpyAsync(d_ztab, ctx->host_stage, sizeof(float) * n_samples, hipMemcpyHostToDevice, s));
+      ctx->up_z = hz;
+      ctx->up_zbuf = ctx->zbuf;
+    }
+    if (need_u) {
+      std::memcpy(ctx->host_stage + 1024, hu.data(), sizeof(float) * n_importance);
+      HIP_TRY(hipMemcpyAsync(d_u, ctx->host_stage + 1024, sizeof(float) * n_importance, hipMemcpyHostToDevice, s));
+      ctx->up_u = hu;
+      ctx->up_wbuf = ctx->wbuf;
+    }
+    HIP_TRY(hipEventRecord(ctx->stage_ev, s));
+  }
 
-  for (bool& b : ctx->stage_ran) b = false;
+  nerf_ctx::Frame& fr = ctx->frames[ctx->n_frames % nerf_ctx::kEvFrames];
+  for (bool& b : fr.ran) b = false;
+  fr.profiled = ctx->profiling;
   auto mark = [&](int i) -> int {
-    if (ctx->profiling) HIP_TRY(hipEventRecord(ctx->ev[i], s));
+    if (ctx->profiling) HIP_TRY(hipEventRecord(fr.ev[i], s));
     return NERF_OK;
   };
   if ((rc = mark(0)) != NERF_OK) return rc;
@@ -365,21 +421,21 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
     z_first = d_zstrat;
     z_first_stride = n_samples;
   }
-  ctx->stage_ran[0] = true;
+  fr.ran[0] = true;
   if ((rc = mark(1)) != NERF_OK) return rc;
   const float* z_main = z_first;
   int z_stride = z_first_stride;
   if (n_importance > 0) {
     SampleSrc src{rays_o, rays_d, z_first, z_first_stride, n_samples, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s));
-    ctx->stage_ran[1] = true;
+    fr.ran[1] = true;
     if ((rc = mark(2)) != NERF_OK) return rc;
     // coarse weights only (the coarse image itself is not an output of render_image)
     HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_first, z_first_stride, rays_d, int(n_rays),
                              n_samples, rgb_out, depth_out, nullptr, d_w, s));
     HIP_TRY(launch_importance(z_first, z_first_stride, d_w, u_rays ? u_rays : d_u, u_rays ? n_importance : 0,
                               int(n_rays), n_samples, n_importance, d_zfine, s));
-    ctx->stage_ran[2] = true;
+    fr.ran[2] = true;
     z_main = d_zfine;
     z_stride = n_fine;
   } else {
@@ -394,7 +450,7 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
     SampleSrc src{rays_o, rays_d, z_main, z_stride, n_fine, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s,
                     fused ? ctx->mlp_out : nullptr));
-    ctx->stage_ran[3] = true;
+    fr.ran[3] = true;
   }
   if ((rc = mark(4)) != NERF_OK) return rc;
   if (fused)
@@ -402,8 +458,9 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   else
     HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_main, z_stride, rays_d, int(n_rays), n_fine,
                              rgb_out, depth_out, nullptr, nullptr, s));
-  ctx->stage_ran[4] = true;
-  HIP_TRY(hipEventRecord(ctx->ev[NERF_N_STAGES], s));
+  fr.ran[4] = true;
+  HIP_TRY(hipEventRecord(fr.ev[NERF_N_STAGES], s));
+  ++ctx->n_frames;
   return NERF_OK;
 }
 

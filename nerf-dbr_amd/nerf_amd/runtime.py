@@ -65,6 +65,7 @@ SIGNATURES = {
     "nerf_ctx_set_profiling": (_c.c_int, [_P, _c.c_int]),
     "nerf_ctx_stage_ms": (_c.c_int, [_P, _FP]),
     "nerf_ctx_set_option": (_c.c_int, [_P, _c.c_int, _c.c_int]),
+    "nerf_ctx_stage_ms_history": (_c.c_int, [_P, _c.c_int, _FP]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -270,6 +271,13 @@ class Device:
     def set_fused_composite(self, enable: bool) -> None:
         """NERF_OPT_FUSED_COMPOSITE: compositing in the bf16/fp8 MLP epilogue (default on)."""
         _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_FUSED_COMPOSITE, 1 if enable else 0))
+
+    def stage_ms_history(self, n: int) -> list:
+        """Per-stage device ms of each of the last n renders (n <= 64), oldest first."""
+        ms = (ctypes.c_float * (n * NERF_N_STAGES))()
+        _check(self.lib.nerf_ctx_stage_ms_history(self._ctx, n, ms))
+        return [dict(zip(STAGES, [float(v) for v in ms[k * NERF_N_STAGES:(k + 1) * NERF_N_STAGES]]))
+                for k in range(n)]
 
     def stage_ms(self) -> dict:
         ms = (ctypes.c_float * NERF_N_STAGES)()

@@ -474,3 +474,24 @@ def test_fused_composite_headline_vs_fp32(r16, r32):
     er, ed = maxabs(rgb16, rgb32.cpu().numpy()), maxabs(d16, d32.cpu().numpy())
     print(f"bf16 fused vs fp32, 800x600x128 rows 292-308: rgb {er:.2e} depth {ed:.2e}")
     assert er < 5e-3 and ed < 2e-2
+
+
+def test_back_to_back_renders_reupload_changed_tables(r16):
+    """nerf_render skips re-uploading an unchanged z table / importance draw (no host
+    synchronisation between frames); a changed table must still be uploaded."""
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][1])
+    a64 = [t.clone() for t in r16.render_image(pose, (40, 30), 64)]
+    a96 = [t.clone() for t in r16.render_image(pose, (40, 30), 96)]
+    for _ in range(3):                                # queued without waiting in between
+        b64 = r16.render_image(pose, (40, 30), 64)
+        b96 = r16.render_image(pose, (40, 30), 96)
+    torch.cuda.synchronize()
+    assert all(torch.equal(x, y) for x, y in zip(a64, b64))
+    assert all(torch.equal(x, y) for x, y in zip(a96, b96))
+    r16.near = 2.5                                    # same S, different table
+    try:
+        c64 = r16.render_image(pose, (40, 30), 64)
+        assert not torch.equal(c64[1], a64[1])
+    finally:
+        r16.near = 2.0
+    assert all(torch.equal(x, y) for x, y in zip(a64, r16.render_image(pose, (40, 30), 64)))
