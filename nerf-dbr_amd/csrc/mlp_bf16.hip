@@ -286,7 +286,9 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
 #endif
   compiler_fence();
   NERF_STAMP(cx, 4 + 3 * g);
+#ifndef NERF_ABLATE_NODMA   // timing experiment: the ring keeps its first chunks (real weights), wrong results
   stage_chunk(cx.blob, (g + kSlots - 1) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
+#endif
 }
 // Conversion schedule (default): layer L's output tiles 2q-2, 2q-1 become final
 // at the end of its quarter q-1 and are converted to the next layer's B
