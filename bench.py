@@ -251,6 +251,7 @@ def main():
         out.update(extra)
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
+        dist.barrier()            # rank 0's extras (error band) finish before any rank tears down
         dist.destroy_process_group()
 
 

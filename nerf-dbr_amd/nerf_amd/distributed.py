@@ -25,10 +25,27 @@ def max_band_rows(world: int, height: int) -> int:
     return max(r1 - r0 for r0, r1 in bands(world, height))
 
 
+_GATHER_BUFS = {}
+
+
+def _gather_buffers(world: int, rows: int, width: int, device):
+    """Send/receive buffers of gather_bands, allocated once per shape and device
+    (a frame loop then launches no allocations)."""
+    import torch
+
+    key = (world, rows, width, str(device))
+    if key not in _GATHER_BUFS:
+        _GATHER_BUFS[key] = (torch.zeros(rows, width, 4, dtype=torch.float32, device=device),
+                             torch.empty(world * rows, width, 4, dtype=torch.float32, device=device))
+    return _GATHER_BUFS[key]
+
+
 def gather_bands(rgb_band, depth_band, width: int, height: int, group=None):
     """All-gather every rank's band into the full (rgb [H,W,3], depth [H,W]) on every rank.
 
-    Bands are padded to the largest band so one ``all_gather_into_tensor`` moves them.
+    Bands are padded to the largest band so one ``all_gather_into_tensor`` moves them
+    (with H divisible by the world size, as 600 rows over 1/2/4/8 GPUs, there is no
+    padding and the gathered buffer is the frame as it stands).
     """
     import torch
     import torch.distributed as dist
@@ -37,10 +54,9 @@ def gather_bands(rgb_band, depth_band, width: int, height: int, group=None):
     rank = dist.get_rank(group)
     r0, r1 = band(rank, world, height)
     rows = max_band_rows(world, height)
-    packed = torch.zeros(rows, width, 4, dtype=torch.float32, device=rgb_band.device)
+    packed, full = _gather_buffers(world, rows, width, rgb_band.device)
     packed[: r1 - r0, :, :3] = rgb_band
     packed[: r1 - r0, :, 3] = depth_band
-    full = torch.empty(world * rows, width, 4, dtype=torch.float32, device=rgb_band.device)
     if packed.is_cuda and dist.get_backend(group) == "gloo":
         # rehearsal of the multi-rank path on one device (gloo has no device
         # all-gather): stage through host memory
@@ -49,9 +65,11 @@ def gather_bands(rgb_band, depth_band, width: int, height: int, group=None):
         full.copy_(host)
     else:
         dist.all_gather_into_tensor(full, packed, group=group)
-    full = full.reshape(world, rows, width, 4)
-    pieces = [full[r, : b1 - b0] for r, (b0, b1) in enumerate(bands(world, height))]
-    img = torch.cat(pieces, 0)
+    if height % world == 0:
+        img = full
+    else:
+        full4 = full.reshape(world, rows, width, 4)
+        img = torch.cat([full4[r, : b1 - b0] for r, (b0, b1) in enumerate(bands(world, height))], 0)
     return img[..., :3].contiguous(), img[..., 3].contiguous()
 
 
