@@ -346,9 +346,10 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   int rc = check_net(ctx, net_main, precision);
   if (rc != NERF_OK) return rc;
   if (n_importance > 0 && (rc = check_net(ctx, NERF_NET_COARSE, precision)) != NERF_OK) return rc;
-  if (!c2w || !t_vals || !rgb_out || !depth_out) return set_error(NERF_E_INVALID, "nerf_render: null argument");
+  if (!c2w || !t_vals) return set_error(NERF_E_INVALID, "nerf_render: null argument");
   if (width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 > row1)
     return set_error(NERF_E_INVALID, "nerf_render: bad image/rows %dx%d [%d,%d)", width, height, row0, row1);
+  if (row1 > row0 && (!rgb_out || !depth_out)) return set_error(NERF_E_INVALID, "nerf_render: null output");
   if (n_samples <= 0 || n_samples > 1024 || n_importance < 0 || n_importance > 1024 ||
       (n_importance > 0 && (n_samples < 2 || n_samples > 256)))
     return set_error(NERF_E_INVALID, "nerf_render: bad sample counts %d+%d", n_samples, n_importance);
