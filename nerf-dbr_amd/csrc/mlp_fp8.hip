@@ -254,7 +254,12 @@ __device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x
   if (kConvert) {
     // per-sample scale: the largest ReLU output of the previous layer -> [128, 256)
     int mb = max_pair(amax, acc[6], acc[7]);
-    mb = __builtin_elementwise_max(mb, __shfl_xor(mb, 32));
+    // the other lane half's maximum: v_permlane32_swap (VALU), not __shfl_xor,
+    // whose ds_bpermute made hipcc drain every in-flight fragment read with
+    // lgkmcnt(0) at each layer start.  Swapping mb with itself leaves, in either
+    // result, each lane's own value in one and its partner's in the other.
+    const auto sw = __builtin_amdgcn_permlane32_swap(mb, mb, false, false);
+    mb = __builtin_elementwise_max(int(sw[0]), int(sw[1]));
     const int e = __builtin_amdgcn_frexp_expf(i2f(mb)) - 8;   // max = f * 2^(e+8), f in [0.5, 1)
     s = __builtin_ldexpf(1.0f, e);
     sb = 127 + e;
