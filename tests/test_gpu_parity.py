@@ -542,3 +542,25 @@ def test_empty_band_and_single_sample(ckpt, precision):
     rgb, depth = r.render_image(pose, (64, 48), 1)
     torch.cuda.synchronize()
     assert float(rgb.abs().max()) == 0.0 and float(depth.abs().max()) == 0.0
+
+
+def test_repeated_renders_do_not_grow_memory(r16):
+    """The reference's memory check (test_system.py:258-287: RSS growth < 500 MB over
+    repeated renders), here for host RSS and device memory: the context's scratch is
+    allocated once per size and reused, so after a warm-up frame neither grows."""
+    import psutil
+
+    pose = torch.eye(4)
+    pose[2, 3] = 4.0
+    r16.render_image(pose, (800, 600), 128)
+    torch.cuda.synchronize()
+    rss0 = psutil.Process().memory_info().rss
+    free0, _ = torch.cuda.mem_get_info()
+    for _ in range(20):
+        r16.render_image(pose, (800, 600), 128)
+    torch.cuda.synchronize()
+    rss_growth = psutil.Process().memory_info().rss - rss0
+    dev_growth = free0 - torch.cuda.mem_get_info()[0]
+    print(f"20 frames 800x600x128: host RSS +{rss_growth / 2**20:.1f} MiB, device +{dev_growth / 2**20:.1f} MiB")
+    assert rss_growth < 500 * 2**20
+    assert dev_growth < 64 * 2**20
