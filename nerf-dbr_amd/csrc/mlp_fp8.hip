@@ -47,7 +47,10 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;           // 256
 constexpr int kUnitB = kFp8UnitBytes;                                // 4 KiB: 2 tiles x 64 lanes x 32 B
 constexpr int kUnits = kFp8Units + kFp8HeadUnits;                    // 134
-constexpr int kChunkUnits = 4;
+#ifndef NERF_FP8_CHUNK_UNITS
+#define NERF_FP8_CHUNK_UNITS 4       // 4 KiB units per LDS chunk (one barrier per chunk)
+#endif
+constexpr int kChunkUnits = NERF_FP8_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitB;                        // 16 KiB
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
 constexpr int kSlots = 4;
