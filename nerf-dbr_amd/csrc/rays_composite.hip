@@ -191,14 +191,63 @@ __global__ __launch_bounds__(64 * kImpWaves) void importance_wave_kernel(
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  double sum = 0.0;
-  for (int i = 0; i < n_coarse; ++i) sum = __dadd_rn(sum, double(a[i]));
-  const float total = float(sum);
-  sum = 0.0;
   if (lane == 0) cdf[0] = 0.0f;
-  for (int i = 0; i < n_coarse; ++i) {
-    sum = __dadd_rn(sum, double(__fdiv_rn(a[i], total)));
-    if ((i & 63) == lane) cdf[i + 1] = float(sum);
+  // Parallel form when it is provably exact.  A double sum of floats is exact in
+  // any order when every partial sum fits in 53 bits: for the normaliser, when
+  // e(max) + ceil(log2 n) - (e(min) - 24) <= 53 (e: frexp exponents, so the
+  // smallest value's last bit is 2^(e(min)-24)); for the cdf (sums < 2), when the
+  // smallest pdf has e >= -28.  Weights in [0, 1] (every composite output) give
+  // spreads far inside both; otherwise every lane runs the sequential sums.
+  const int per = (n_coarse + 63) >> 6;                       // elements per lane, contiguous
+  const int i0 = min(lane * per, n_coarse), i1 = min(i0 + per, n_coarse);
+  float amin = __builtin_inff(), amax = 0.0f;
+  bool finite_pos = true;
+  for (int i = i0; i < i1; ++i) {
+    finite_pos = finite_pos && a[i] > 0.0f && a[i] < __builtin_inff();
+    amin = fminf(amin, a[i]);
+    amax = fmaxf(amax, a[i]);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    amin = fminf(amin, __shfl_xor(amin, d));
+    amax = fmaxf(amax, __shfl_xor(amax, d));
+  }
+  int log2n = 0;
+  while ((1 << log2n) < n_coarse) ++log2n;
+  bool exact = __all(finite_pos) &&
+               __builtin_amdgcn_frexp_expf(amax) + log2n - (__builtin_amdgcn_frexp_expf(amin) - 24) <= 53;
+  if (exact) {
+    double loc = 0.0;
+    for (int i = i0; i < i1; ++i) loc = __dadd_rn(loc, double(a[i]));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) loc = __dadd_rn(loc, __shfl_xor(loc, d));
+    const float total = float(loc);
+    exact = __builtin_amdgcn_frexp_expf(__fdiv_rn(amin, total)) >= -28;   // wave-uniform (amin, total are)
+    if (exact) {
+      double part = 0.0;
+      for (int i = i0; i < i1; ++i) part = __dadd_rn(part, double(__fdiv_rn(a[i], total)));
+      double incl = part;                                     // inclusive scan over lanes
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(incl, d);
+        if (lane >= d) incl = __dadd_rn(incl, o);
+      }
+      double run = __dsub_rn(incl, part);                     // exclusive: exact, so no rounding
+      for (int i = i0; i < i1; ++i) {
+        run = __dadd_rn(run, double(__fdiv_rn(a[i], total)));
+        cdf[i + 1] = float(run);
+      }
+    }
+  }
+  if (!exact) {
+    double sum = 0.0;
+    for (int i = 0; i < n_coarse; ++i) sum = __dadd_rn(sum, double(a[i]));
+    const float total = float(sum);
+    sum = 0.0;
+    for (int i = 0; i < n_coarse; ++i) {
+      sum = __dadd_rn(sum, double(__fdiv_rn(a[i], total)));
+      if ((i & 63) == lane) cdf[i + 1] = float(sum);
+    }
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -564,3 +564,25 @@ def test_repeated_renders_do_not_grow_memory(r16):
     print(f"20 frames 800x600x128: host RSS +{rss_growth / 2**20:.1f} MiB, device +{dev_growth / 2**20:.1f} MiB")
     assert rss_growth < 500 * 2**20
     assert dev_growth < 64 * 2**20
+
+
+@pytest.mark.parametrize("s,kind", [(64, "unit"), (7, "unit"), (200, "unit"), (256, "unit"),
+                                    (64, "wide"), (200, "wide")])
+def test_importance_sampler_exact_paths(r32, s, kind):
+    """The sampler's normaliser and cdf are torch-CPU cumsums (sequential double).
+    The kernel sums in parallel when that is provably exact (weights in [0, 1], the
+    composite's range: kind "unit") and sequentially otherwise (kind "wide": weights
+    spanning 1e-30..1e6); both must equal the oracle bit for bit."""
+    from oracle import nerf_oracle as O
+
+    torch.manual_seed(11 + s)
+    n, ni = 97, 130
+    z = torch.sort(torch.rand(n, s) * 4.0 + 2.0, -1).values.contiguous()
+    w = torch.rand(n, s) ** 3
+    if kind == "wide":
+        w = w * torch.pow(10.0, torch.randint(-30, 7, (n, s)).float())
+    w[3] = 0.0
+    u = torch.sort(torch.rand(n, ni), -1).values.contiguous()
+    ref = O.fine_z(z, w, u)
+    got = r32.importance_sample(z, w, u)
+    assert np.array_equal(got.cpu().numpy(), ref.numpy())
