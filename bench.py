@@ -100,6 +100,40 @@ def other_configs(ckpt, pose, local, ref32):
     return out
 
 
+def sharded_hierarchical(ckpt, pose, local, rank, world, width, height, n_warm=2, n_steps=5):
+    """C4: 64 coarse + 128 importance samples, bf16, each rank its row band, one
+    all-gather per frame; rays/s of the whole frame over the slowest rank."""
+    import torch
+    import torch.distributed as dist
+
+    from nerf_amd import distributed as D
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    h = MI355XRenderer("bf16", n_importance=128, device_index=local)
+    h.setup(ckpt)
+    r0, r1 = D.band(rank, world, height)
+    rgb_b = torch.empty(r1 - r0, width, 3, device="cuda")
+    dep_b = torch.empty(r1 - r0, width, device="cuda")
+
+    def step():
+        h.render_rows(pose, (width, height), 64, r0, r1, rgb_b, dep_b)
+        D.gather_bands(rgb_b, dep_b, width, height)
+
+    for _ in range(n_warm):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n_steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = D.reduce_max(time.perf_counter() - t0) / n_steps
+    return {"rays_per_s": width * height / dt, "ms_per_frame": 1e3 * dt, "n_gpus": world,
+            "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)",
+            "parallelism": f"row-band x{world} + {dist.get_backend()} all-gather"}
+
+
 def cpu_baseline(pose, width, height, spp, target_s):
     """Oracle (PyTorch CPU) on a band of rows of the same frame; ~target_s seconds of CPU work."""
     import torch
@@ -198,6 +232,10 @@ def main():
     peak = PEAK_TFLOPS[args.precision]
 
     extra = {}
+    if world > 1 and not args.no_extras:
+        # BASELINE config 4: the 64+128 hierarchical frame (bf16), sharded in row
+        # bands over every rank and all-gathered -- every rank takes part
+        extra["c4_hierarchical_sharded"] = sharded_hierarchical(ckpt, pose, local, rank, world, width, height)
     ref = None
     if rank == 0 and ((args.precision != "fp32" and not args.no_error_check) or (world == 1 and not args.no_extras)):
         ref = MI355XRenderer("fp32", device_index=local)

@@ -428,7 +428,7 @@ def test_multi_rank_rehearsal_on_one_device():
     out = js.loads(line)
     assert out["world"] == 2 and out["identical"]
     res = _torchrun([os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--width", "200",
-                     "--height", "150", "--spp", "32", "--cpu-seconds", "0", "--no-error-check", "--no-extras"],
+                     "--height", "150", "--spp", "32", "--cpu-seconds", "0", "--no-error-check"],
                     {"NERF_DIST_BACKEND": "gloo"})
     assert res.returncode == 0, res.stderr[-3000:]
     # exactly one JSON line, from rank 0 (gloo's own connection messages aside)
@@ -436,6 +436,8 @@ def test_multi_rank_rehearsal_on_one_device():
     assert len(lines) == 1, res.stdout
     b = js.loads(lines[0])
     assert b["n_gpus"] == 2 and b["value"] > 0 and b["config"]["parallelism"].startswith("row-band x2")
+    c4 = b["c4_hierarchical_sharded"]                 # config 4, every rank taking part
+    assert c4["n_gpus"] == 2 and c4["rays_per_s"] > 0
 
 
 # ------------------------------------- compositing fused into the MLP epilogue --
