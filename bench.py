@@ -151,9 +151,16 @@ def cpu_baseline(pose, width, height, spp, target_s):
     t0 = time.time()
     O.render_image(net, pose, (width, height), spp, rows=(r0, r0 + rows))
     dt = time.time() - t0
+    cpu = "unknown CPU"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": rows * width / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle render_image rows [{r0},{r0 + rows}) of {width}x{height}x{spp} "
-                      f"({rows * width} rays, {dt:.1f} s, 512-ray chunks, torch {torch.__version__})"}
+                      f"({rows * width} rays, {dt:.1f} s, 512-ray chunks, torch {torch.__version__}, "
+                      f"{torch.get_num_threads()} threads on {cpu})"}
 
 
 def main():
