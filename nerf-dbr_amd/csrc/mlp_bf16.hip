@@ -83,8 +83,13 @@ constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 10
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kCols * 4 * 1024;
 constexpr int kLdsSegOff = kLdsDeOff + kWaves * kCols * 2 * 1024;       // fused compositing: (dist, z) per sample
 constexpr int kLdsStampOff = kLdsSegOff + kWaves * kCols * kSamplesPerWave * 8;
+#ifdef NERF_ABLATE_DMASINK   // timing experiment: restaging lands in a chunk nobody reads
+constexpr int kLdsSinkOff = kLdsStampOff;
+#endif
 #ifdef NERF_STAMPS
 constexpr int kLdsBytes = kLdsStampOff + kWaves * (2 + 3 * kTotalChunks + 1) * 8;
+#elif defined(NERF_ABLATE_DMASINK)
+constexpr int kLdsBytes = kLdsStampOff + kChunkB;
 #else
 constexpr int kLdsBytes = kLdsStampOff;
 #endif
@@ -121,6 +126,9 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
   const char* src = blob + size_t(g) * kChunkB + wave_u * 1024 + lane * 16;
 #endif
   char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
+#ifdef NERF_ABLATE_DMASINK
+  if (g >= kSlots) dst = lds + kLdsSinkOff + wave_u * 1024;   // the ring keeps its first fill
+#endif
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i) {
 #ifdef NERF_BF16_BUILTIN_GLDS
@@ -434,7 +442,11 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   // Start the weight stream (chunks 0 .. kSlots-3; each tile's top stages one
   // more) and copy the parameters, once per workgroup.
 #pragma unroll
+#if defined(NERF_ABLATE_NODMA) || defined(NERF_ABLATE_DMASINK)
+  for (int g = 0; g < kSlots; ++g) stage_chunk(blob, g, lds, wave_u, lane);   // every slot real weights
+#else
   for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+#endif
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   const float* prm = (const float*)(lds + kLdsParamOff);
