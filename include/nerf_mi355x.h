@@ -169,11 +169,13 @@ int nerf_ctx_stage_ms(nerf_ctx* ctx, float* ms_out /* [NERF_N_STAGES] */);
 int nerf_ctx_stage_ms_history(nerf_ctx* ctx, int n, float* ms_out /* [n][NERF_N_STAGES] */);
 
 /* Context options (no reference counterpart: implementation switches of this library).
- *   NERF_OPT_FUSED_COMPOSITE (default 1): in nerf_render / nerf_render_sampled, bf16 and
- *   fp8 passes whose per-ray sample count is a multiple of 32 composite inside the MLP
- *   kernel (per-32-sample partial integrals, chained per ray; the same sums as
+ *   NERF_OPT_FUSED_COMPOSITE, a bit mask (default 3): in nerf_render / nerf_render_sampled,
+ *   bf16 and fp8 passes whose per-ray sample count is a multiple of 32 composite inside the
+ *   MLP kernel (per-32-sample partial integrals, chained per ray; the same sums as
  *   execute_volume_rendering, src/benchmark/pytorch_renderers.py:105-125, regrouped).
- *   0 writes (sigma, rgb) per sample and runs the sequential composite kernel. */
+ *   Bit 1: the rendered pass (uniform, or the hierarchical fine pass); bit 2: the
+ *   hierarchical coarse pass, whose weights then come from the MLP epilogue. 0 writes
+ *   (sigma, rgb) per sample and runs the sequential composite kernel for both. */
 #define NERF_OPT_FUSED_COMPOSITE 1
 int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value);
 

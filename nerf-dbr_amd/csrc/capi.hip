@@ -70,7 +70,7 @@ struct nerf_ctx {
   const float* up_wbuf = nullptr;
   hipEvent_t stage_ev = nullptr; // recorded after the last upload from host_stage
   bool profiling = false;
-  bool fused_composite = true; // NERF_OPT_FUSED_COMPOSITE
+  int fused_composite = 3;     // NERF_OPT_FUSED_COMPOSITE bits: 1 render passes, 2 hierarchical coarse pass
   // stage events of the last kEvFrames renders (a ring, so that per-frame stage
   // times can be read after a run of back-to-back renders without a host sync each)
   struct Frame {
@@ -119,10 +119,10 @@ struct DeviceGuard {
 };
 
 hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, long n, float* out, bool expl,
-                   hipStream_t s, float* seg = nullptr) {
+                   hipStream_t s, float* seg = nullptr, float* wloc = nullptr) {
   const NetDev& nd = ctx->net[net];
-  if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg);
-  if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg);
+  if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg, wloc);
+  if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg, wloc);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
 }
 
@@ -298,7 +298,8 @@ int nerf_ctx_set_profiling(nerf_ctx* ctx, int enable) {
 int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value) {
   if (!ctx) return set_error(NERF_E_INVALID, "null context");
   if (option == NERF_OPT_FUSED_COMPOSITE) {
-    ctx->fused_composite = value != 0;
+    if (value < 0 || value > 3) return set_error(NERF_E_INVALID, "NERF_OPT_FUSED_COMPOSITE takes 0..3, got %d", value);
+    ctx->fused_composite = value;
     return NERF_OK;
   }
   return set_error(NERF_E_INVALID, "unknown option %d", option);
@@ -427,15 +428,24 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   const float* z_main = z_first;
   int z_stride = z_first_stride;
   if (n_importance > 0) {
+    // bf16 / fp8 coarse pass with whole segments: the weights come out of the MLP
+    // epilogue (in-segment weight per sample + the segment records) and the
+    // sampler scales them by the earlier segments' transmittance; otherwise the
+    // (sigma, rgb) buffer and the sequential composite kernel (the coarse image
+    // itself is not an output of render_image)
+    const bool fuse_coarse = (ctx->fused_composite & 2) && precision != NERF_FP32 && n_samples % 32 == 0 &&
+                             n_importance <= 1024;
     SampleSrc src{rays_o, rays_d, z_first, z_first_stride, n_samples, nullptr, nullptr};
-    HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s));
+    HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s,
+                    fuse_coarse ? ctx->mlp_out : nullptr, fuse_coarse ? d_w : nullptr));
     fr.ran[1] = true;
     if ((rc = mark(2)) != NERF_OK) return rc;
-    // coarse weights only (the coarse image itself is not an output of render_image)
-    HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_first, z_first_stride, rays_d, int(n_rays),
-                             n_samples, rgb_out, depth_out, nullptr, d_w, s));
+    if (!fuse_coarse)
+      HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_first, z_first_stride, rays_d, int(n_rays),
+                               n_samples, rgb_out, depth_out, nullptr, d_w, s));
     HIP_TRY(launch_importance(z_first, z_first_stride, d_w, u_rays ? u_rays : d_u, u_rays ? n_importance : 0,
-                              int(n_rays), n_samples, n_importance, d_zfine, s));
+                              int(n_rays), n_samples, n_importance, d_zfine, s,
+                              fuse_coarse ? ctx->mlp_out : nullptr));
     fr.ran[2] = true;
     z_main = d_zfine;
     z_stride = n_fine;
@@ -446,7 +456,7 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   // bf16 / fp8 with whole 32-sample segments per ray: compositing fused into the
   // MLP epilogue (one record per segment), then chained per ray; the fp32 parity
   // path keeps the sequential composite kernel
-  const bool fused = ctx->fused_composite && precision != NERF_FP32 && n_fine > 1 && n_fine % 32 == 0;
+  const bool fused = (ctx->fused_composite & 1) && precision != NERF_FP32 && n_fine > 1 && n_fine % 32 == 0;
   {
     SampleSrc src{rays_o, rays_d, z_main, z_stride, n_fine, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s,

@@ -408,8 +408,9 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
 // (sigma, r, g, b) of a tile's samples, or with fused compositing (seg) each
 // column's segment record (nerf_device.h SegRecord, lanes 0 and 1); p0 < 0:
 // nothing pending
-__device__ __forceinline__ void store_results(const f32x4 (&res)[kCols], long p0, long n_points, int lane,
-                                              f32x4* __restrict__ out, f32x4* __restrict__ seg) {
+__device__ __forceinline__ void store_results(const f32x4 (&res)[kCols], const float (&wl)[kCols], long p0,
+                                              long n_points, int lane, f32x4* __restrict__ out,
+                                              f32x4* __restrict__ seg, float* __restrict__ wloc) {
   if (p0 < 0) return;
 #pragma unroll
   for (int c = 0; c < kCols; ++c) {
@@ -417,6 +418,7 @@ __device__ __forceinline__ void store_results(const f32x4 (&res)[kCols], long p0
     if (seg) {
       const long first = p - (lane & 31);                 // the segment's first sample
       if (first < n_points && lane < 2) seg[(first / kSamplesPerWave) * 2 + lane] = res[c];
+      if (wloc != nullptr && p < n_points && lane < 32) wloc[p] = wl[c];
     } else if (p < n_points && lane < 32) {
       out[p] = res[c];
     }
@@ -427,7 +429,7 @@ template <bool kExplicit>
 __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __restrict__ blob,
                                                                const float* __restrict__ prm_g, SampleSrc src,
                                                                long n_points, f32x4* __restrict__ out,
-                                                               f32x4* __restrict__ seg) {
+                                                               f32x4* __restrict__ seg, float* __restrict__ wloc) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -455,6 +457,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   // vmcnt counts stores with the LDS-DMA in issue order, so a store issued last
   // would make the next tile's first wait also wait out the store.
   f32x4 res[kCols];
+  float wl[kCols];
   long res_p0 = -1;
 
 #pragma unroll 1
@@ -505,7 +508,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     __syncthreads();
     stage_chunk(cx.blob, kSlots - 2, lds, wave_u, lane);
     NERF_STAMP(cx, 1);
-    store_results(res, res_p0, n_points, lane, out, seg);
+    store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
     f32x16 acc[kCols][8];
 #pragma unroll
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       res[c] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
       if (!kExplicit && seg != nullptr) {
         const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + ((wave_u * kCols + c) * kSamplesPerWave + (lane & 31)) * 8);
-        res[c] = seg_composite(res[c], in[0], in[1], lane);
+        res[c] = seg_composite(res[c], in[0], in[1], lane, wl[c]);
       }
     }
     res_p0 = p0;
@@ -589,7 +592,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
         g_nerf_stamps[tile - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
 #endif
   }
-  store_results(res, res_p0, n_points, lane, out, seg);
+  store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
   // the stream ran kSlots-2 chunks into a tile that does not exist: let them
   // land before the workgroup's LDS is released
   wait_vmcnt(0);
@@ -598,7 +601,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 }  // namespace
 
 hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                           bool explicit_points, hipStream_t stream, float* seg) {
+                           bool explicit_points, hipStream_t stream, float* seg, float* wloc) {
   if (n_points <= 0) return hipSuccess;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 #ifdef NERF_BF16_ONE_TILE
@@ -610,10 +613,10 @@ hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSr
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)
     hipLaunchKernelGGL(mlp_bf16_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out, (f32x4*)seg);
+                       (f32x4*)out, (f32x4*)seg, wloc);
   else
     hipLaunchKernelGGL(mlp_bf16_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out, (f32x4*)seg);
+                       (f32x4*)out, (f32x4*)seg, wloc);
   return hipGetLastError();
 }
 

@@ -318,7 +318,7 @@ template <bool kExplicit>
 __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __restrict__ blob,
                                                               const float* __restrict__ prm_g, SampleSrc src,
                                                               long n_points, f32x4* __restrict__ out,
-                                                              f32x4* __restrict__ seg) {
+                                                              f32x4* __restrict__ seg, float* __restrict__ wloc) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -431,9 +431,11 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   const f32x4 res{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
   if (!kExplicit && seg != nullptr) {                  // fused compositing: one record per segment
     const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane_o & 31)) * 8);
-    const f32x4 rec = seg_composite(res, in[0], in[1], lane_o);
+    float wl;
+    const f32x4 rec = seg_composite(res, in[0], in[1], lane_o, wl);
     const long first = p_o - (lane_o & 31);
     if (first < n_points && lane_o < 2) seg[(first / kSamplesPerWave) * 2 + lane_o] = rec;
+    if (wloc != nullptr && p_o < n_points && h == 0) wloc[p_o] = wl;
   } else if (p_o < n_points && h == 0) {
     out[p_o] = res;
   }
@@ -442,17 +444,17 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
 }  // namespace
 
 hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                          bool explicit_points, hipStream_t stream, float* seg) {
+                          bool explicit_points, hipStream_t stream, float* seg, float* wloc) {
   if (n_points <= 0) return hipSuccess;
   const long blocks = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)
     hipLaunchKernelGGL(mlp_fp8_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out, (f32x4*)seg);
+                       (f32x4*)out, (f32x4*)seg, wloc);
   else
     hipLaunchKernelGGL(mlp_fp8_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out, (f32x4*)seg);
+                       (f32x4*)out, (f32x4*)seg, wloc);
   return hipGetLastError();
 }
 

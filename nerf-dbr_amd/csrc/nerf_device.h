@@ -316,12 +316,16 @@ __device__ __forceinline__ float lane31(float v) {
 
 // Composite the segment held by lanes 0..31 (sample j of the segment in lane j;
 // lanes 32..63 scan their own copy, which no caller stores).  v = (sigma, r, g, b).
-// Returns this lane's 16 B of the record (even lanes: P, r, g; odd: b, depth, acc, 0).
-__device__ __forceinline__ f32x4 seg_composite(f32x4 v, float dist, float z, int lane) {
+// Returns this lane's 16 B of the record (even lanes: P, r, g; odd: b, depth, acc, 0)
+// and, in w_local, its sample's in-segment weight alpha * float(P_<j) (the
+// hierarchical coarse pass turns it into the sample's weight with the product of
+// the earlier segments' P: importance_wave_kernel).
+__device__ __forceinline__ f32x4 seg_composite(f32x4 v, float dist, float z, int lane, float& w_local) {
   const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-relu(v[0]), dist)));
   const double P = seg_scan_mul(double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
   const double Pex = dpp_f64<0x138>(P, 1.0);                   // exclusive: lane j takes lane j-1, lane 0 1.0
   const float w = __fmul_rn(alpha, float(Pex));
+  w_local = w;
   const float r = lane31(seg_scan_add(__fmul_rn(w, v[1])));
   const float g = lane31(seg_scan_add(__fmul_rn(w, v[2])));
   const float b = lane31(seg_scan_add(__fmul_rn(w, v[3])));

@@ -20,11 +20,14 @@ hipError_t launch_generate_rays(const float* c2w_rowmajor16, int width, int heig
 hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSrc& src, long n_points,
                           float* out, bool explicit_points, hipStream_t stream);
 // seg (render passes with n_samples % 32 == 0 only): compositing fused into the
-// epilogue, one 32-B SegRecord per 32-sample segment instead of out's (sigma, rgb)
+// epilogue, one 32-B SegRecord per 32-sample segment instead of out's (sigma, rgb);
+// wloc (with seg): each sample's in-segment weight as well (hierarchical coarse pass)
 hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSrc& src, long n_points,
-                           float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr);
+                           float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr,
+                           float* wloc = nullptr);
 hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points,
-                          float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr);
+                          float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr,
+                          float* wloc = nullptr);
 // Chains each ray's segment records into (rgb, depth) (nerf_device.h SegRecord).
 hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
                                      hipStream_t stream);
@@ -34,8 +37,10 @@ hipError_t launch_composite(const float* sigma, int sigma_stride, const float* r
                             hipStream_t stream);
 hipError_t launch_sample(const float* z_tab, const float* t_rand, int n_rays, int n_samples, const float* rays_o,
                          const float* rays_d, float* z_out, float* points_out, hipStream_t stream);
+// seg (optional): weights are in-segment weights of a fused coarse pass, scaled
+// here by the product of the ray's earlier segment records' P
 hipError_t launch_importance(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
                              int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine,
-                             hipStream_t stream);
+                             hipStream_t stream, const float* seg = nullptr);
 
 }  // namespace nerf

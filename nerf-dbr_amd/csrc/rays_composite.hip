@@ -145,6 +145,7 @@ __global__ void importance_kernel(const float* __restrict__ z_coarse, int z_ray_
 //    the sequential merge's order whenever both lists are nondecreasing (true for
 //    sorted z and ascending u); otherwise lane 0 merges sequentially.
 constexpr int kMaxImpWave = 1024;
+constexpr int kSegSamples = 32;     // samples per segment record (nerf_device.h SegRecord)
 constexpr int kImpWaves = 4;
 
 __device__ __forceinline__ int count_le(const float* a, int n, float v) {   // #{i < n : a[i] <= v}
@@ -169,7 +170,7 @@ __device__ __forceinline__ int count_lt(const float* a, int n, float v) {   // #
 __global__ __launch_bounds__(64 * kImpWaves) void importance_wave_kernel(
     const float* __restrict__ z_coarse, int z_ray_stride, const float* __restrict__ weights,
     const float* __restrict__ u, int u_ray_stride, int n_rays, int n_coarse, int n_importance,
-    float* __restrict__ z_fine) {
+    float* __restrict__ z_fine, const SegRecord* __restrict__ seg) {
   __shared__ float s_a[kImpWaves][kMaxCoarse];
   __shared__ float s_cdf[kImpWaves][kMaxCoarse + 1];
   __shared__ float s_z[kImpWaves][kMaxCoarse];
@@ -186,7 +187,16 @@ __global__ __launch_bounds__(64 * kImpWaves) void importance_wave_kernel(
   float* zc = s_z[wv];
   float* zs = s_zs[wv];
   for (int i = lane; i < n_coarse; i += 64) {
-    a[i] = __fadd_rn(wr[i], 1e-5f);
+    float w = wr[i];
+    if (seg != nullptr) {
+      // fused coarse pass: w is the in-segment weight; the transmittance at the
+      // segment's start is the product of the earlier records' P (double)
+      const SegRecord* sr = seg + r * (n_coarse / kSegSamples);
+      double T = 1.0;
+      for (int k = 0; k < i / kSegSamples; ++k) T = __dmul_rn(T, sr[k].P);
+      w = __fmul_rn(w, float(T));
+    }
+    a[i] = __fadd_rn(w, 1e-5f);
     zc[i] = zr[i];
   }
   __builtin_amdgcn_wave_barrier();
@@ -439,13 +449,13 @@ hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segment
 
 hipError_t launch_importance(const float* z_coarse, int z_ray_stride, const float* weights, const float* u,
                              int u_ray_stride, int n_rays, int n_coarse, int n_importance, float* z_fine,
-                             hipStream_t stream) {
+                             hipStream_t stream, const float* seg) {
   if (n_rays <= 0) return hipSuccess;
   if (n_coarse > kMaxCoarse) return hipErrorInvalidValue;
   if (n_importance <= kMaxImpWave) {
     const dim3 grid{unsigned((n_rays + kImpWaves - 1) / kImpWaves), 1, 1}, block{64 * kImpWaves, 1, 1};
     hipLaunchKernelGGL(importance_wave_kernel, grid, block, 0, stream, z_coarse, z_ray_stride, weights, u,
-                       u_ray_stride, n_rays, n_coarse, n_importance, z_fine);
+                       u_ray_stride, n_rays, n_coarse, n_importance, z_fine, (const SegRecord*)seg);
     return hipGetLastError();
   }
   const int threads = 64;

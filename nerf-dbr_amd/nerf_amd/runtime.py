@@ -268,9 +268,11 @@ class Device:
     def set_profiling(self, enable: bool) -> None:
         _check(self.lib.nerf_ctx_set_profiling(self._ctx, 1 if enable else 0))
 
-    def set_fused_composite(self, enable: bool) -> None:
-        """NERF_OPT_FUSED_COMPOSITE: compositing in the bf16/fp8 MLP epilogue (default on)."""
-        _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_FUSED_COMPOSITE, 1 if enable else 0))
+    def set_fused_composite(self, enable, coarse: bool = True) -> None:
+        """NERF_OPT_FUSED_COMPOSITE: compositing in the bf16/fp8 MLP epilogue (default on),
+        for the rendered pass and (``coarse``) the hierarchical coarse pass's weights."""
+        _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_FUSED_COMPOSITE,
+                                            (1 if enable else 0) | (2 if enable and coarse else 0)))
 
     def stage_ms_history(self, n: int) -> list:
         """Per-stage device ms of each of the last n renders (n <= 64), oldest first."""

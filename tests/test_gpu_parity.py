@@ -455,8 +455,8 @@ def test_fused_composite_matches_sequential(ckpt, precision, spp, n_imp):
     pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
     res = (67, 41)                                  # ragged: the last MLP tile is partial
     r.hip.set_fused_composite(False)
-    rgb_s, d_s = r.render_image(pose, res, spp)
-    r.hip.set_fused_composite(True)
+    rgb_s, d_s = [t.clone() for t in r.render_image(pose, res, spp)]
+    r.hip.set_fused_composite(True, coarse=False)         # the rendered pass only
     rgb_f, d_f = r.render_image(pose, res, spp)
     er, ed = maxabs(rgb_f, rgb_s.cpu().numpy()), maxabs(d_f, d_s.cpu().numpy())
     print(f"fused vs sequential composite {precision} {spp}+{n_imp}: rgb {er:.2e} depth {ed:.2e}")
@@ -464,6 +464,15 @@ def test_fused_composite_matches_sequential(ckpt, precision, spp, n_imp):
         assert er == 0.0 and ed == 0.0
     else:
         assert er < 1e-5 and ed < 1e-5 * 6.0
+    if n_imp:
+        # also the coarse pass: its weights move at rounding level, which moves the
+        # importance samples slightly (amplified by the 2^9*pi encoding of the fine
+        # pass), so the bound is the hierarchical end-to-end one
+        r.hip.set_fused_composite(True, coarse=True)
+        rgb_c, d_c = r.render_image(pose, res, spp)
+        ec, edc = maxabs(rgb_c, rgb_s.cpu().numpy()), maxabs(d_c, d_s.cpu().numpy())
+        print(f"  + fused coarse weights: rgb {ec:.2e} depth {edc:.2e}")
+        assert ec < 2e-2 and edc < 2e-2
 
 
 def test_fused_composite_headline_vs_fp32(r16, r32):
