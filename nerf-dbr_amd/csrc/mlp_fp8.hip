@@ -9,6 +9,7 @@
 // of the next, 8 waves x 32 samples, quarter schedule, an LDS ring filled by
 // LDS-DMA with one barrier per chunk, asm fragment reads with counted waits.
 // What differs:
+//   * waves 4-7 run one chunk behind waves 0-3 (NERF_FP8_LAG below);
 //   * k-steps are 64 wide: a hidden k-step takes accumulator tiles 2u, 2u+1;
 //     a 256-wide layer has 4 k-steps (vs 16 in bf16), each MFMA is 64 cycles
 //     and does 4x the work of a bf16 one, at twice the bf16 FLOP rate;
@@ -53,12 +54,30 @@ constexpr int kUnits = kFp8Units + kFp8HeadUnits;                    // 134
 constexpr int kChunkUnits = NERF_FP8_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitB;                        // 16 KiB
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
-constexpr int kSlots = 4;
+#ifndef NERF_FP8_SLOTS
+#define NERF_FP8_SLOTS 4
+#endif
+constexpr int kSlots = NERF_FP8_SLOTS;
+// Wave lag (default; -DNERF_FP8_LAG=0 for lockstep): waves 4-7 run one chunk
+// behind waves 0-3, so the two waves of a SIMD reach their layer boundaries
+// (scale reduction and conversion, nothing for the MFMA pipe) at different
+// times.  The ring then holds one chunk more for the lagging half: every wave
+// stages one chunk less far ahead, and the lagging half's seam g is barrier
+// instance g + 1 (one extra barrier at its start, one at the leading half's
+// end).  Measured -1.6 % kernel time, bit-identical output; a 5-slot ring
+// (restoring the staging distance) was slower (-1.1 %).
+#ifndef NERF_FP8_LAG
+#define NERF_FP8_LAG 1
+#endif
+constexpr int kLagOn = NERF_FP8_LAG;
+static_assert(kLagOn == 0 || kSlots >= 4, "a lagged ring needs 4 slots");
 constexpr int kPf = 2;                                               // fragment prefetch distance (units)
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);
 static_assert(kTotalChunks * kChunkB <= kFp8ScaleOff, "ring reads stay inside the padded fragment area");
-static_assert(kSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
+// slots 0-3 are read at ring_addr + offset, a fifth at ring_hi_addr (ds_read offsets are 16 bits)
+constexpr int kLoSlots = 65536 / kChunkB;
+static_assert(kSlots <= kLoSlots + 1 && kLoSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
 constexpr int kLdsParamOff = kSlots * kChunkB;
 constexpr int kLdsScaleOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
 constexpr int kLdsPeOff = kLdsScaleOff + kFp8ScaleBytes;
@@ -106,13 +125,18 @@ struct Ctx {
   char* lds;
   int wave_u, lane, h;
   unsigned ring_addr, pe_addr, bias_addr, scale_addr;   // direction slots: pe_addr + kDeFromPe
+  unsigned ring_hi_addr;                                 // ring slot kLoSlots (5-slot ring only)
+  int lag;                                               // 1: this wave runs a chunk behind (NERF_FP8_LAG)
 };
 
-__device__ __forceinline__ void stage_chunk(const Ctx& cx, int g) {
-  char* dst = cx.lds + (g % kSlots) * kChunkB + cx.wave_u * 1024;
+// Stage chunk g + lag (g a constant after unrolling, lag wave-uniform 0 or 1).
+__device__ __forceinline__ void stage_chunk(const Ctx& cx, int g, int lag = 0) {
+  const int s0 = g % kSlots;
+  const int slot = s0 + lag == kSlots ? 0 : s0 + lag;
+  char* dst = cx.lds + slot * kChunkB + cx.wave_u * 1024;
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i)
-    lds_dma_16_s(cx.blob + size_t(g) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
+    lds_dma_16_s(cx.blob + size_t(g + lag) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
                  lds_addr(dst + i * kThreads * 16));
 }
 
@@ -125,11 +149,22 @@ NL_HD int dma_outstanding_at_seam(int g) {
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
   const int g = (n + kPf) / kChunkUnits - 1;
-  wait_vmcnt(kGldsPerStage * dma_outstanding_at_seam(g));
+  if (kLagOn) {
+    // own pieces of chunk g+1+lag landed: stages younger than it are those of
+    // chunks up to g+lag+kSlots-3 (one fewer near the end; a smaller count only waits longer)
+    int younger = kSlots - 4 < kTotalChunks - 3 - g ? kSlots - 4 : kTotalChunks - 3 - g;
+    wait_vmcnt(kGldsPerStage * (younger > 0 ? younger : 0));
+  } else {
+    wait_vmcnt(kGldsPerStage * dma_outstanding_at_seam(g));
+  }
   compiler_fence();
   __builtin_amdgcn_s_barrier();
   compiler_fence();
-  if (g + kSlots - 1 < kTotalChunks) stage_chunk(cx, g + kSlots - 1);
+  if (kLagOn) {
+    if (g + cx.lag + kSlots - 2 < kTotalChunks) stage_chunk(cx, g + kSlots - 2, cx.lag);
+  } else if (g + kSlots - 1 < kTotalChunks) {
+    stage_chunk(cx, g + kSlots - 1);
+  }
 }
 
 __device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
@@ -139,11 +174,13 @@ __device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
 // Unit n -> ring entry n % kRing: two A fragments (32 B per lane each, as two
 // lane-linear 16-B halves) and, for an encoding k-step, the B fragment.
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing]) {
-  const int off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
+  const int slot = (n / kChunkUnits) % kSlots;
+  const unsigned addr = slot < kLoSlots ? cx.ring_addr : cx.ring_hi_addr;
+  const int off = (slot < kLoSlots ? slot : 0) * kChunkB + (n % kChunkUnits) * kUnitB;
 #pragma unroll
   for (int o2 = 0; o2 < 2; ++o2)
-    ra[n % kRing][o2] = join(ds_read_b128<i32x4>(cx.ring_addr, off + o2 * 2048),
-                             ds_read_b128<i32x4>(cx.ring_addr, off + o2 * 2048 + 1024));
+    ra[n % kRing][o2] = join(ds_read_b128<i32x4>(addr, off + o2 * 2048),
+                             ds_read_b128<i32x4>(addr, off + o2 * 2048 + 1024));
   const int ex = unit_extra(n);
   if (ex != 0) {
     const int eo = ex == kPos ? 0 : kDeFromPe;
@@ -328,11 +365,13 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
                base + lane * 16,
                base + kLdsPeOff + wave_u * 2048 + lane * 16,
                base + kLdsParamOff + h * 64,
-               base + kLdsScaleOff + lane * 8};
+               base + kLdsScaleOff + lane * 8,
+               base + kLoSlots * kChunkB + lane * 16,
+               kLagOn && wave_u >= kWaves / 2 ? 1 : 0};
   const long p = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
 
 #pragma unroll
-  for (int g = 0; g < kSlots - 1; ++g) stage_chunk(cx, g);
+  for (int g = 0; g < kSlots - 1 - kLagOn; ++g) stage_chunk(cx, g);
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   for (int i = threadIdx.x; i < kFp8ScaleBytes / 16; i += kThreads)
@@ -365,8 +404,17 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
       if (h == 0) *(f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane & 31)) * 8) = f32x2_t{dist, zz};
     }
   }
-  wait_vmcnt(kGldsPerStage * (kSlots - 2));            // chunk 0 landed (own pieces)
+  wait_vmcnt(kGldsPerStage * (kSlots - 2 - kLagOn));   // chunk 0 landed (own pieces)
   __syncthreads();
+  if (kLagOn && cx.lag) {
+    // the lagging half's extra seam (barrier instance 0): its pieces of chunk 1
+    // landed, then chunk kSlots-2 staged, as the leading half does at its seam 0
+    wait_vmcnt(kGldsPerStage * (kSlots - 4));
+    compiler_fence();
+    __builtin_amdgcn_s_barrier();
+    compiler_fence();
+    stage_chunk(cx, kSlots - 2);
+  }
   i32x8 ra[kRing][2], rb[kRing];
 #pragma unroll
   for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
@@ -422,6 +470,12 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
                                                         hacc, 0, 0, 0);
       }
     }
+  }
+  if (kLagOn && !cx.lag) {
+    // the leading half's matching barrier for the lagging half's last seam
+    compiler_fence();
+    __builtin_amdgcn_s_barrier();
+    compiler_fence();
   }
   // the sample index again, from the lane id recounted by v_mbcnt: keeping the
   // 64-bit p (or the lane id) live through the layers costs a spill, and its
