@@ -67,6 +67,12 @@ constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
 #ifndef NERF_BF16_PF
 #define NERF_BF16_PF 2               // fragment prefetch distance (units)
 #endif
+// Wave lag (-DNERF_BF16_LAG=1, lab): waves 4-7 run one chunk behind waves 0-3
+// (the fp8 kernel's scheme, mlp_fp8.hip); needs a ring of >= 4 slots.
+#ifndef NERF_BF16_LAG
+#define NERF_BF16_LAG 0
+#endif
+constexpr int kLagOn = NERF_BF16_LAG;
 constexpr int kUnits = kHeadUnitBase + kHeadUnits;                   // 516 layer units + 12 head units
 constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitBytes;
@@ -76,7 +82,7 @@ constexpr int kPf = NERF_BF16_PF;
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // LDS-DMA pieces per wave per chunk
 constexpr int kLdsParamOff = kSlots * kChunkB;
-static_assert(kSlots >= 3 && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
+static_assert(kSlots >= 3 + kLagOn && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
 static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile: chunk g of every tile uses slot g % kSlots");
 static_assert(kTotalChunks * kChunkB <= kBf16BlobBytes, "device blob is padded for every chunk geometry");
 constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
@@ -119,13 +125,17 @@ NL_HD int unit_extra(int n) {   // 0: B from hidden fragments (or head units); e
 
 // Chunk g -> ring slot g % kSlots.  Each wave moves its share as lane-linear
 // 1 KiB LDS-DMA pieces (destination = wave-uniform base + lane*16).
-__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
+__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane,
+                                            int lag = 0) {
+  // lag (wave-uniform 0/1): chunk g + lag of the cyclic stream, in its slot
+  const int gl = g + lag == kTotalChunks ? 0 : g + lag;
+  const int slot = g % kSlots + lag == kSlots ? 0 : g % kSlots + lag;
 #ifdef NERF_ABLATE_HOTCHUNK   // timing experiment: every chunk re-reads chunk 0 (L2-hot, wrong results)
   const char* src = blob + wave_u * 1024 + lane * 16;
 #else
   const char* src = blob + size_t(g) * kChunkB + wave_u * 1024 + lane * 16;
 #endif
-  char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
+  char* dst = lds + slot * kChunkB + wave_u * 1024;
 #ifdef NERF_ABLATE_DMASINK
   if (g >= kSlots) dst = lds + kLdsSinkOff + wave_u * 1024;   // the ring keeps its first fill
 #endif
@@ -141,7 +151,7 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
     lds_dma_16(src + i * kThreads * 16, lds_addr(dst + i * kThreads * 16));
 #else
     (void)src;
-    lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
+    lds_dma_16_s(blob + size_t(gl) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
                  lds_addr(dst + i * kThreads * 16));
 #endif
 #endif
@@ -208,6 +218,7 @@ struct Ctx {
   // direction encodings, and of this lane half's bias rows (asm reads add an
   // immediate offset)
   unsigned ring_addr, pe_addr, de_addr, bias_addr;
+  int lag;   // NERF_BF16_LAG: 1 for waves 4-7
 };
 
 #ifndef NERF_BF16_CC_LDS
@@ -281,7 +292,8 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
 //   (3) stage chunk g+kSlots-1 into chunk g-1's slot -- past the end of the
 //       tile, the next tile's chunk of the same slot.
 // The top of a tile is seam E_-1 (tile_top).
-constexpr int kDmaOutstandingAtSeam = kSlots - 3;
+constexpr int kDmaOutstandingAtSeam = kSlots - 3 - kLagOn;
+constexpr int kStageAhead = kSlots - 1 - kLagOn;   // seam g stages chunk g + kStageAhead (+ the wave's lag)
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
   const int g = (n + kPf) / kChunkUnits - 1;
@@ -295,7 +307,7 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   compiler_fence();
   NERF_STAMP(cx, 4 + 3 * g);
 #ifndef NERF_ABLATE_NODMA   // timing experiment: the ring keeps its first chunks (real weights), wrong results
-  stage_chunk(cx.blob, (g + kSlots - 1) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
+  stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane, cx.lag);
 #endif
 }
 // Conversion schedule (default): layer L's output tiles 2q-2, 2q-1 become final
@@ -438,7 +450,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16,
                lds_base + kLdsPeOff + wave_u * kCols * 4096 + lane * 16,
                lds_base + kLdsDeOff + wave_u * kCols * 2048 + lane * 16,
-               lds_base + kLdsParamOff + h * 64};
+               lds_base + kLdsParamOff + h * 64, kLagOn && wave_u >= kWaves / 2 ? 1 : 0};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
   // Start the weight stream (chunks 0 .. kSlots-3; each tile's top stages one
@@ -447,11 +459,17 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 #if defined(NERF_ABLATE_NODMA) || defined(NERF_ABLATE_DMASINK)
   for (int g = 0; g < kSlots; ++g) stage_chunk(blob, g, lds, wave_u, lane);   // every slot real weights
 #else
-  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+  for (int g = 0; g < kSlots - 2 - kLagOn; ++g) stage_chunk(blob, g, lds, wave_u, lane);
 #endif
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   const float* prm = (const float*)(lds + kLdsParamOff);
+  if (kLagOn && cx0.lag) {
+    // the lagging half's extra seam (the leading half's first tile top): chunk 0 landed, publish, stage
+    wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
+    __syncthreads();
+    stage_chunk(blob, kStageAhead - 1, lds, wave_u, lane);
+  }
 
   // A tile's results are stored at the top of the next tile, after its seam:
   // vmcnt counts stores with the LDS-DMA in issue order, so a store issued last
@@ -506,7 +524,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     // previous chunk every wave finished with the last tile.
     wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
-    stage_chunk(cx.blob, kSlots - 2, lds, wave_u, lane);
+    stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane, cx.lag);
     NERF_STAMP(cx, 1);
     store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
@@ -592,6 +610,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
         g_nerf_stamps[tile - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
 #endif
   }
+  if (kLagOn && !cx0.lag) __builtin_amdgcn_s_barrier();   // the lagging half's last seam
   store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
   // the stream ran kSlots-2 chunks into a tile that does not exist: let them
   // land before the workgroup's LDS is released
