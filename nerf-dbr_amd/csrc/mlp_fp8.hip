@@ -415,6 +415,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     compiler_fence();
     stage_chunk(cx, kSlots - 2);
   }
+#if defined(NERF_FP8_PRIO)   // lab: static priority 1 for waves 4-7 (1) or 0-3 (2)
+  if ((NERF_FP8_PRIO == 1) == (wave_u >= kWaves / 2)) __builtin_amdgcn_s_setprio(1);
+#endif
   i32x8 ra[kRing][2], rb[kRing];
 #pragma unroll
   for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
