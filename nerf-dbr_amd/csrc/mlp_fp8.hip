@@ -160,11 +160,13 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   compiler_fence();
   __builtin_amdgcn_s_barrier();
   compiler_fence();
+#ifndef NERF_FP8_ABLATE_NODMA   // timing experiment: the ring keeps its first fill (wrong results)
   if (kLagOn) {
     if (g + cx.lag + kSlots - 2 < kTotalChunks) stage_chunk(cx, g + kSlots - 2, cx.lag);
   } else if (g + kSlots - 1 < kTotalChunks) {
     stage_chunk(cx, g + kSlots - 1);
   }
+#endif
 }
 
 __device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
@@ -228,6 +230,15 @@ __device__ __forceinline__ int relu_e4m3x4(int w) {
 // (byte j: register j&15 of tile 2u + (j>>4)), divided by the sample's
 // activation scale s, converted, then ReLU'd on the bytes.
 __device__ __forceinline__ void convert_pair(const f32x16& t0, const f32x16& t1, i32x8& b, float s) {
+#if defined(NERF_FP8_ABLATE_CONVERT)   // timing experiment: raw accumulator bits, no VALU (wrong results)
+  (void)s;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    b[d] = f2i(t0[4 * d]);
+    b[4 + d] = f2i(t1[4 * d]);
+  }
+  return;
+#endif
 #ifdef NERF_FP8_RELU_F32
   // previous form: ReLU on the fp32 bit patterns, one v_max_i32 per value
   float v[32];
@@ -266,6 +277,9 @@ __device__ __forceinline__ void colour_dword(const f32x16 (&acc)[8], int t, int 
 // negative int32 and non-negative floats order like their bits, so a signed
 // integer max started at 0 is max(relu(x)) -- v_max3_i32, no NaN canonicalising.
 __device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t1) {
+#ifdef NERF_FP8_ABLATE_MAX   // timing experiment: no running maximum (wrong scales)
+  return m ^ f2i(t0[0]) ^ f2i(t1[15]);
+#endif
   // chained as max(max(m, a), b) so each pair folds into one v_max3_i32
 #pragma unroll
   for (int i = 0; i < 16; i += 2)
@@ -371,7 +385,11 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   const long p = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
 
 #pragma unroll
+#ifdef NERF_FP8_ABLATE_NODMA
+  for (int g = 0; g < kSlots; ++g) stage_chunk(cx, g);   // every slot real weights
+#else
   for (int g = 0; g < kSlots - 1 - kLagOn; ++g) stage_chunk(cx, g);
+#endif
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   for (int i = threadIdx.x; i < kFp8ScaleBytes / 16; i += kThreads)
@@ -413,7 +431,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     compiler_fence();
     __builtin_amdgcn_s_barrier();
     compiler_fence();
+#ifndef NERF_FP8_ABLATE_NODMA
     stage_chunk(cx, kSlots - 2);
+#endif
   }
 #if defined(NERF_FP8_PRIO)   // lab: static priority 1 for waves 4-7 (1) or 0-3 (2)
   if ((NERF_FP8_PRIO == 1) == (wave_u >= kWaves / 2)) __builtin_amdgcn_s_setprio(1);
