@@ -597,3 +597,25 @@ def test_importance_sampler_exact_paths(r32, s, kind):
     ref = O.fine_z(z, w, u)
     got = r32.importance_sample(z, w, u)
     assert np.array_equal(got.cpu().numpy(), ref.numpy())
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+@pytest.mark.parametrize("res,s", [((1, 1), 32), ((17, 5), 64), ((33, 9), 100), ((7, 3), 2)])
+def test_ragged_shapes_reduced_precision(ckpt, r32, precision, res, s):
+    """Partial 256-sample tiles and partial 32-sample segments on the bf16 / fp8
+    MLPs (fused compositing when S % 32 == 0, the sequential path otherwise),
+    against the fp32 parity path on the same pose, with the tolerances of the
+    full-size tests (test_render_bf16_error_bounded, test_render_fp8_error_vs_fp32)."""
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    r = MI355XRenderer(precision)
+    r.setup(ckpt)
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
+    rgb, depth = r.render_image(pose, res, s)
+    rgb32, d32 = r32.render_image(pose, res, s)
+    assert rgb.shape == (res[1], res[0], 3) and depth.shape == (res[1], res[0])
+    assert torch.isfinite(rgb).all() and torch.isfinite(depth).all()
+    er, ed = maxabs(rgb, rgb32.cpu().numpy()), maxabs(depth, d32.cpu().numpy())
+    mr = float((rgb.cpu() - rgb32.cpu()).abs().mean())
+    print(f"{precision} {res}x{s}: rgb max {er:.3e} mean {mr:.3e}, depth max {ed:.3e}")
+    assert er < 0.1 and ed < 0.5 and mr < 0.01
