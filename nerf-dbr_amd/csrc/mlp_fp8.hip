@@ -71,7 +71,10 @@ constexpr int kSlots = NERF_FP8_SLOTS;
 #endif
 constexpr int kLagOn = NERF_FP8_LAG;
 static_assert(kLagOn == 0 || kSlots >= 4, "a lagged ring needs 4 slots");
-constexpr int kPf = 2;                                               // fragment prefetch distance (units)
+#ifndef NERF_FP8_PF
+#define NERF_FP8_PF 1   // 1: 224 VGPRs, -1.0 % against 2 (256 VGPRs); 3 spills
+#endif
+constexpr int kPf = NERF_FP8_PF;                                     // fragment prefetch distance (units)
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);
 static_assert(kTotalChunks * kChunkB <= kFp8ScaleOff, "ring reads stay inside the padded fragment area");
