@@ -15,12 +15,12 @@
 //     and does 4x the work of a bf16 one, at twice the bf16 FLOP rate;
 //   * weights are e4m3 with a power-of-two (E8M0) scale per output row, chosen
 //     at packing so no row saturates; the MFMA applies it (scale_a operand);
-//   * activations are e4m3 with a per-sample power-of-two scale: a sample's
-//     largest ReLU output of the previous layer maps into [128, 256), so
-//     nothing can overflow to NaN (e4m3fn has no infinity); the MFMA applies
-//     the scale back (scale_b).  The running maximum is gathered during the
-//     previous layer's quarters, so only its last two tiles are reduced at the
-//     layer boundary;
+//   * activations are e4m3 with a power-of-two scale per sample and 64-row
+//     block (one k-step of the next layer): the block's largest ReLU output
+//     maps into [128, 256), so nothing can overflow to NaN (e4m3fn has no
+//     infinity, and the conversion does not saturate); the MFMA applies the
+//     scale back (scale_b, per k-step).  A block is converted as soon as its
+//     two tiles are final, one block per quarter (layer_fp8b);
 //   * encodings are e4m3 at scale 1 (|sin|,|cos| <= 1; positions clamped to
 //     +-448).
 //   * heads as one more MFMA tile (nerf_layout.h kFp8HeadUnits): the density
@@ -66,6 +66,9 @@ constexpr int kSlots = NERF_FP8_SLOTS;
 // instance g + 1 (one extra barrier at its start, one at the leading half's
 // end).  Measured -1.6 % kernel time, bit-identical output; a 5-slot ring
 // (restoring the staging distance) was slower (-1.1 %).
+#ifndef NERF_FP8_BLOCK_SCALES
+#define NERF_FP8_BLOCK_SCALES 1     // per-sample scale per 64-row activation block (layer_fp8b); 0: one per sample
+#endif
 #ifndef NERF_FP8_LAG
 #define NERF_FP8_LAG 1
 #endif
@@ -293,6 +296,91 @@ __device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t
   return m;
 }
 
+#if NERF_FP8_BLOCK_SCALES
+// Block scales: one activation scale per sample per 64-row block, i.e. per k-step
+// of the next layer (tiles 2v, 2v+1 -> k-step v).  Block v's scale is known as
+// soon as its two tiles are final, so a layer converts its own output one block
+// per quarter (quarters 1-3: blocks 0-2, the next layer's quarter 0: block 3)
+// into the other fragment set, and no layer waits for its whole predecessor.
+__device__ __forceinline__ int block_scale(const f32x16& t0, const f32x16& t1, float& s) {
+  int mb = max_pair(0, t0, t1);
+  const auto sw = __builtin_amdgcn_permlane32_swap(mb, mb, false, false);
+  mb = __builtin_elementwise_max(int(sw[0]), int(sw[1]));
+  const int e = __builtin_amdgcn_frexp_expf(i2f(mb)) - 8;   // max = f * 2^(e+8), f in [0.5, 1)
+  s = __builtin_ldexpf(1.0f, e);
+  return 127 + e;
+}
+__device__ __forceinline__ void convert_tile(const f32x16& t, i32x8& b, int off, float s) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) b[off + d] = relu_e4m3x4(cvt4_scaled(t[4 * d], t[4 * d + 1], t[4 * d + 2], t[4 * d + 3], s));
+}
+
+// Layer L reads bin (its hidden k-steps, scales sin) and writes its own output
+// into bout / sout; C0 converts its tiles 0, 1 to the colour fragments hb[0..3]
+// during quarter 1.
+template <int L>
+__device__ __forceinline__ void layer_fp8b(f32x16 (&acc)[8], i32x8 (&bin)[4], i32x8 (&bout)[4], int (&sin)[4],
+                                           int (&sout)[4], i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing],
+                                           u32x4 (&hb)[8], const Ctx& cx) {
+  constexpr LayerShape sh = layer_shape(L);
+  constexpr int KH = sh.hidden / 64;
+  constexpr int KU = ksteps_fp8(L);
+  constexpr int NQ = out_tiles(L) / 2;
+  constexpr int N0 = fp8_unit_base(L);
+  constexpr bool kPrev = L != L0;        // the previous layer's block 3 (tiles 6, 7) -> bin[3] in quarter 0
+  constexpr bool kNext = L != C0;        // this layer's blocks 0-2 -> bout in quarters 1-3
+  constexpr int U0 = 0, U1 = KU >= 3 ? 1 : 0, U2 = KU >= 3 ? 2 : 0;   // scale, first tile, second tile
+  static_assert(!kPrev || KH == 4, "block 3 is converted before k-step 3 reads it");
+  float s_pend = 1.0f;
+  int sa0 = 127, sa1 = 127;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int n = N0 + q * KU + u;
+      seam_before(cx, n);
+      if (u == 0) {
+#pragma unroll
+        for (int o2 = 0; o2 < 2; ++o2) {
+          const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
+          const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
+          const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
+          acc[2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                   b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+        }
+        const u32x2 sc = ds_read_b64(cx.scale_addr, (L * 4 + q) * 512);
+        sa0 = int(sc[0]);
+        sa1 = int(sc[1]);
+      }
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      wait_lgkm(lgkm_for_unit(n));
+      const bool hidden = u < KH;
+      const i32x8 b = hidden ? bin[hidden ? u : 0] : rb[n % kRing];
+      const int sbu = hidden ? sin[hidden ? u : 0] : 127;
+      acc[2 * q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][0], b, acc[2 * q], 0, 0, 0, sa0, 0,
+                                                                  sbu);
+      acc[2 * q + 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][1], b, acc[2 * q + 1], 0, 0, 0,
+                                                                      sa1, 0, sbu);
+      if (kPrev && q == 0) {
+        if (u == U0) sin[3] = block_scale(acc[6], acc[7], s_pend);
+        if (u == U1) convert_tile(acc[6], bin[3], 0, s_pend);
+        if (u == U2) convert_tile(acc[7], bin[3], 4, s_pend);
+      }
+      if (kNext && q >= 1) {
+        if (u == U0) sout[q >= 1 ? q - 1 : 0] = block_scale(acc[2 * q - 2], acc[2 * q - 1], s_pend);
+        if (u == U1) convert_tile(acc[2 * q - 2], bout[q >= 1 ? q - 1 : 0], 0, s_pend);
+        if (u == U2) convert_tile(acc[2 * q - 1], bout[q >= 1 ? q - 1 : 0], 4, s_pend);
+      }
+      if (L == C0 && q == 1) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if ((m * KU) / 16 == u) colour_dword(acc, 0, m, hb);
+      }
+    }
+  }
+}
+#endif
+
 // (C0 also leaves its activation scale in sb_out for the density k-steps and
 // converts its tiles 0, 1 to the colour fragments hb[0..3] during quarter 1.)
 template <int L>
@@ -446,8 +534,23 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
 
   f32x16 acc[8];
-  i32x8 bh[4];
   u32x4 hb[8];
+#if NERF_FP8_BLOCK_SCALES
+  // two fragment sets: layer l reads one while it fills the other for l+1
+  i32x8 bA[4], bB[4];
+  int sA[4] = {127, 127, 127, 127}, sB[4] = {127, 127, 127, 127};
+  layer_fp8b<L0>(acc, bB, bA, sB, sA, ra, rb, hb, cx);
+  layer_fp8b<L1>(acc, bA, bB, sA, sB, ra, rb, hb, cx);
+  layer_fp8b<L2>(acc, bB, bA, sB, sA, ra, rb, hb, cx);
+  layer_fp8b<L3>(acc, bA, bB, sA, sB, ra, rb, hb, cx);
+  layer_fp8b<L4>(acc, bB, bA, sB, sA, ra, rb, hb, cx);   // skip: [x, pe] (nerf.py:109-110)
+  layer_fp8b<L5>(acc, bA, bB, sA, sB, ra, rb, hb, cx);
+  layer_fp8b<L6>(acc, bB, bA, sB, sA, ra, rb, hb, cx);
+  layer_fp8b<L7>(acc, bA, bB, sA, sB, ra, rb, hb, cx);
+  layer_fp8b<C0>(acc, bB, bA, sB, sA, ra, rb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+  i32x8 (&bh)[4] = bB;                                   // C0's input: the density k-steps
+#else
+  i32x8 bh[4];
   int amax = 0, sb = 127;
   layer_fp8<L0>(acc, bh, ra, rb, amax, sb, hb, cx);
   layer_fp8<L1>(acc, bh, ra, rb, amax, sb, hb, cx);
@@ -458,6 +561,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   layer_fp8<L6>(acc, bh, ra, rb, amax, sb, hb, cx);
   layer_fp8<L7>(acc, bh, ra, rb, amax, sb, hb, cx);
   layer_fp8<C0>(acc, bh, ra, rb, amax, sb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+#endif
 
   // Heads (nerf.py:114, 123-129) as one MFMA tile: row 3 density (fp8 k-steps
   // over bh, C0's input, at C0's activation scale), rows 0-2 colour (bf16
@@ -481,8 +585,13 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     if (i < kFp8DensityUnits) {
 #pragma unroll
       for (int o2 = 0; o2 < 2; ++o2)
+#if NERF_FP8_BLOCK_SCALES
+        hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
+                                                               0, sB[2 * i + o2]);
+#else
         hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
                                                                0, sb);
+#endif
 #pragma unroll
       for (int m = 0; m < 16; ++m)
         if (m / 8 == i) colour_dword(acc, 2, m, hb);

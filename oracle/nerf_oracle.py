@@ -253,8 +253,9 @@ def render_image_hierarchical(coarse: Net, fine: Net, c2w, resolution: Tuple[int
 # defined here, as the kernel computes it (mlp_fp8.hip), in float64:
 #   * weights: e4m3 (RNE) of W / 2^e_r, e_r the smallest power of two with
 #     max|W_r| / 2^e_r <= 448, per output row r;
-#   * activations (previous layer's ReLU output): e4m3 of x / 2^e_s, per sample,
-#     e_s = frexp exponent of the sample's largest value - 8 (range [128, 256));
+#   * activations (previous layer's ReLU output): e4m3 of x / 2^e, one e per
+#     sample per 64-row block (rows 64v..64v+63 are the next layer's k-step v),
+#     e = frexp exponent of the block's largest value - 8 (range [128, 256));
 #   * encodings: e4m3 at scale 1; bias and accumulation in full precision;
 #   * heads (nerf_layout.h kFp8HeadUnits): density as one more fp8 row over C0's
 #     quantised input (its own row scale), colour in bf16 (weights and ReLU'd
@@ -273,8 +274,12 @@ def bf16_round(x):
 
 
 def fp8_activation_exponent(x):
-    m = np.maximum(x, 0).max(axis=0)
-    return np.frexp(m.astype(np.float32))[1].astype(np.int64) - 8
+    """x [rows, n] (rows a multiple of 64) -> per-row exponents [rows, n]: each
+    64-row block of a sample shares its block's scale (mlp_fp8.hip layer_fp8b)."""
+    rows, n = x.shape
+    m = np.maximum(x, 0).reshape(rows // 64, 64, n).max(axis=1)
+    e = np.frexp(m.astype(np.float32))[1].astype(np.int64) - 8
+    return np.repeat(e, 64, axis=0)
 
 
 def fp8_weight_rows(w):
