@@ -73,6 +73,13 @@ constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
 #define NERF_BF16_LAG 0
 #endif
 constexpr int kLagOn = NERF_BF16_LAG;
+// Deferred compositing (-DNERF_BF16_DEFER_COMP=1, lab): a tile's segment
+// composite (seg_composite) runs at the top of the next tile, after its seam,
+// instead of in the epilogue before the next tile's encodings.
+#ifndef NERF_BF16_DEFER_COMP
+#define NERF_BF16_DEFER_COMP 0
+#endif
+constexpr bool kDeferComp = NERF_BF16_DEFER_COMP;
 constexpr int kUnits = kHeadUnitBase + kHeadUnits;                   // 516 layer units + 12 head units
 constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitBytes;
@@ -476,6 +483,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   // would make the next tile's first wait also wait out the store.
   f32x4 res[kCols];
   float wl[kCols];
+  f32x2_t segin[kCols];   // kDeferComp: the pending tile's (dist, z) per column
   long res_p0 = -1;
 
 #pragma unroll 1
@@ -526,6 +534,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     __syncthreads();
     stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane, cx.lag);
     NERF_STAMP(cx, 1);
+    if (kDeferComp && !kExplicit && seg != nullptr && res_p0 >= 0)
+#pragma unroll
+      for (int c = 0; c < kCols; ++c) res[c] = seg_composite(res[c], segin[c][0], segin[c][1], lane, wl[c]);
     store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
     f32x16 acc[kCols][8];
@@ -592,7 +603,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       res[c] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
       if (!kExplicit && seg != nullptr) {
         const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + ((wave_u * kCols + c) * kSamplesPerWave + (lane & 31)) * 8);
-        res[c] = seg_composite(res[c], in[0], in[1], lane, wl[c]);
+        if (kDeferComp) segin[c] = in;
+        else res[c] = seg_composite(res[c], in[0], in[1], lane, wl[c]);
       }
     }
     res_p0 = p0;
@@ -611,6 +623,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 #endif
   }
   if (kLagOn && !cx0.lag) __builtin_amdgcn_s_barrier();   // the lagging half's last seam
+  if (kDeferComp && !kExplicit && seg != nullptr && res_p0 >= 0)
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) res[c] = seg_composite(res[c], segin[c][0], segin[c][1], lane, wl[c]);
   store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
   // the stream ran kSlots-2 chunks into a tile that does not exist: let them
   // land before the workgroup's LDS is released
