@@ -303,6 +303,11 @@ __device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t
 // per quarter (quarters 1-3: blocks 0-2, the next layer's quarter 0: block 3)
 // into the other fragment set, and no layer waits for its whole predecessor.
 __device__ __forceinline__ int block_scale(const f32x16& t0, const f32x16& t1, float& s) {
+#ifdef NERF_FP8_ABLATE_STATIC   // timing experiment: a fixed scale (1.0), no maximum (static-scale contract)
+  (void)t0; (void)t1;
+  s = 1.0f;
+  return 127;
+#endif
   int mb = max_pair(0, t0, t1);
   const auto sw = __builtin_amdgcn_permlane32_swap(mb, mb, false, false);
   mb = __builtin_elementwise_max(int(sw[0]), int(sw[1]));
@@ -311,6 +316,14 @@ __device__ __forceinline__ int block_scale(const f32x16& t0, const f32x16& t1, f
   return 127 + e;
 }
 __device__ __forceinline__ void convert_tile(const f32x16& t, i32x8& b, int off, float s) {
+#ifdef NERF_FP8_ABLATE_STATIC   // ReLU and saturation as one v_med3_f32 per value, then the plain convert
+  const float hi = kFp8Max * s;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+    b[off + d] = cvt4_scaled(__builtin_amdgcn_fmed3f(t[4 * d], 0.0f, hi), __builtin_amdgcn_fmed3f(t[4 * d + 1], 0.0f, hi),
+                             __builtin_amdgcn_fmed3f(t[4 * d + 2], 0.0f, hi), __builtin_amdgcn_fmed3f(t[4 * d + 3], 0.0f, hi), s);
+  return;
+#endif
 #pragma unroll
   for (int d = 0; d < 4; ++d) b[off + d] = relu_e4m3x4(cvt4_scaled(t[4 * d], t[4 * d + 1], t[4 * d + 2], t[4 * d + 3], s));
 }
