@@ -73,13 +73,15 @@ constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
 #define NERF_BF16_LAG 0
 #endif
 constexpr int kLagOn = NERF_BF16_LAG;
-// Deferred compositing (-DNERF_BF16_DEFER_COMP=1, lab): a tile's segment
+// Deferred compositing (-DNERF_BF16_DEFER_COMP=1 or 2, lab): a tile's segment
 // composite (seg_composite) runs at the top of the next tile, after its seam,
-// instead of in the epilogue before the next tile's encodings.
+// (1) or beside the first MFMAs of its L0 (2), instead of in the epilogue
+// before the next tile's encodings.
 #ifndef NERF_BF16_DEFER_COMP
 #define NERF_BF16_DEFER_COMP 0
 #endif
-constexpr bool kDeferComp = NERF_BF16_DEFER_COMP;
+constexpr int kDeferComp = NERF_BF16_DEFER_COMP;   // 1: after the seam; 2: beside L0's first MFMAs
+static_assert(kCols + 1 < 4, "the deferred composite fits L0's first quarter");
 constexpr int kUnits = kHeadUnitBase + kHeadUnits;                   // 516 layer units + 12 head units
 constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitBytes;
@@ -353,9 +355,15 @@ __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (
 }
 #endif
 
-template <int L>
+struct NoHook {
+  __device__ __forceinline__ void operator()(int, int) const {}
+};
+
+// hook(q, u): extra VALU work issued after unit (q, u)'s MFMAs (NERF_BF16_DEFER_COMP=2)
+template <int L, class Hook = NoHook>
 __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[kCols][16], u32x4 (&bout)[kCols][16],
-                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], const Ctx& cx) {
+                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], const Ctx& cx,
+                                           const Hook& hook = Hook{}) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
   constexpr int KU = ksteps_bf16(L);
@@ -409,6 +417,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
         for (int c = 0; c < kCols; ++c)
           acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][o2], b[c], acc[c][2 * q + o2],
                                                                       0, 0, 0);
+      hook(q, u);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
@@ -534,10 +543,10 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     __syncthreads();
     stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane, cx.lag);
     NERF_STAMP(cx, 1);
-    if (kDeferComp && !kExplicit && seg != nullptr && res_p0 >= 0)
+    if (kDeferComp == 1 && !kExplicit && seg != nullptr && res_p0 >= 0)
 #pragma unroll
       for (int c = 0; c < kCols; ++c) res[c] = seg_composite(res[c], segin[c][0], segin[c][1], lane, wl[c]);
-    store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
+    if (kDeferComp != 2 || kExplicit || seg == nullptr) store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
     f32x16 acc[kCols][8];
 #pragma unroll
@@ -545,7 +554,19 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 
     // two B-fragment sets: layer l reads one while it fills the other for l+1
     u32x4 bA[kCols][16], bB[kCols][16];
-    layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
+    if constexpr (kDeferComp == 2 && !kExplicit) {
+      // the previous tile's composite, one column per unit beside L0 quarter 0's
+      // MFMAs (L0 converts nothing there), then its stores
+      const bool pend = seg != nullptr && res_p0 >= 0;
+      auto hook = [&](int q, int u) {
+        if (q == 0 && u >= 1 && u <= kCols && pend)
+          res[u - 1] = seg_composite(res[u - 1], segin[u - 1][0], segin[u - 1][1], lane, wl[u - 1]);
+        if (q == 0 && u == kCols + 1 && seg != nullptr) store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
+      };
+      layer_bf16<L0>(acc, bB, bA, ra, rb, cx, hook);
+    } else {
+      layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
+    }
     layer_bf16<L1>(acc, bA, bB, ra, rb, cx);
     layer_bf16<L2>(acc, bB, bA, ra, rb, cx);
     layer_bf16<L3>(acc, bA, bB, ra, rb, cx);
@@ -603,7 +624,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       res[c] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
       if (!kExplicit && seg != nullptr) {
         const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + ((wave_u * kCols + c) * kSamplesPerWave + (lane & 31)) * 8);
-        if (kDeferComp) segin[c] = in;
+        if (kDeferComp != 0) segin[c] = in;
         else res[c] = seg_composite(res[c], in[0], in[1], lane, wl[c]);
       }
     }
@@ -623,7 +644,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 #endif
   }
   if (kLagOn && !cx0.lag) __builtin_amdgcn_s_barrier();   // the lagging half's last seam
-  if (kDeferComp && !kExplicit && seg != nullptr && res_p0 >= 0)
+  if (kDeferComp != 0 && !kExplicit && seg != nullptr && res_p0 >= 0)
 #pragma unroll
     for (int c = 0; c < kCols; ++c) res[c] = seg_composite(res[c], segin[c][0], segin[c][1], lane, wl[c]);
   store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
