@@ -440,6 +440,37 @@ def test_multi_rank_rehearsal_on_one_device():
     assert c4["n_gpus"] == 2 and c4["rays_per_s"] > 0
 
 
+def test_bench_single_gpu_json_contract():
+    """bench.py at N=1 (reduced frame, bounded CPU sample): one JSON line with the
+    driver's keys, a roofline object for the MLP kernel and a cpu_baseline object;
+    value = W*H*steps / wall time and roofline.frac = achieved / peak."""
+    import json as js
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "3", "--warmup", "1",
+                          "--width", "160", "--height", "120", "--spp", "32", "--cpu-seconds", "0.5",
+                          "--no-error-check", "--no-extras"], capture_output=True, text=True, timeout=110)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    b = js.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in b, k
+    assert b["n_gpus"] == 1 and b["steps"] == 3 and b["warmup"] == 1 and b["dtype"] == "bf16"
+    assert b["higher_is_better"] is True and b["vs_baseline"] is None and "workload" in b["config"]
+    assert b["value"] == pytest.approx(160 * 120 / (b["ms_per_step"] * 1e-3), rel=1e-6)
+    rf = b["roofline"]
+    assert rf["bound"] == "mfma" and rf["unit"] == "TFLOP/s" and rf["peak"] == 2500.0
+    assert 0 < rf["achieved"] and rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"])
+    assert rf["flop_per_launch"] == 160 * 120 * 32 * W.FLOPS_PER_SAMPLE
+    assert rf["traffic"] is None                      # PMC bytes are quoted for the headline frame only
+    cb = b["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["unit"] == "rays/s" and cb["value"] > 0 and cb["cores"] >= 1
+
+
 # ------------------------------------- compositing fused into the MLP epilogue --
 @pytest.mark.parametrize("precision,spp,n_imp", [("bf16", 32, 0), ("bf16", 128, 0), ("bf16", 64, 128),
                                                  ("fp8", 128, 0), ("fp8", 64, 128), ("bf16", 48, 0)])
