@@ -243,6 +243,15 @@ def main():
         # BASELINE config 4: the 64+128 hierarchical frame (bf16), sharded in row
         # bands over every rank and all-gathered -- every rank takes part
         extra["c4_hierarchical_sharded"] = sharded_hierarchical(ckpt, pose, local, rank, world, width, height)
+        # per-frame breakdown at N GPUs: the slowest rank's MLP kernel
+        # and the exchange alone (the step's packing copies + all-gather), 10 frames
+        barrier()
+        t_x = time.perf_counter()
+        for _ in range(10):
+            D.gather_bands(rgb_b, dep_b, width, height)
+        barrier()
+        extra["exchange_ms_per_frame"] = 1e3 * D.reduce_max(time.perf_counter() - t_x) / 10
+        extra["mlp_ms_per_frame_rank_max"] = D.reduce_max(kern_ms)
     ref = None
     if rank == 0 and ((args.precision != "fp32" and not args.no_error_check) or (world == 1 and not args.no_extras)):
         ref = MI355XRenderer("fp32", device_index=local)

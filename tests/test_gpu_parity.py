@@ -438,6 +438,7 @@ def test_multi_rank_rehearsal_on_one_device():
     assert b["n_gpus"] == 2 and b["value"] > 0 and b["config"]["parallelism"].startswith("row-band x2")
     c4 = b["c4_hierarchical_sharded"]                 # config 4, every rank taking part
     assert c4["n_gpus"] == 2 and c4["rays_per_s"] > 0
+    assert b["exchange_ms_per_frame"] > 0 and b["mlp_ms_per_frame_rank_max"] > 0
 
 
 def test_bench_single_gpu_json_contract():
