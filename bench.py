@@ -4,14 +4,18 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 is launched by torch.distributed.run, one process per GPU (RCCL).  A step is one
 ``render_image`` of the full 800x600 frame at 128 uniform samples per ray on the
 fine network (the reference benchmark's semantics, ``benchmark_suite.py:151-235``;
-rays/s = W*H / time, ``:216-220``).  With N GPUs each rank renders its row band and
-the bands are all-gathered over RCCL (strong scaling: the frame is fixed).
+rays/s = W*H / time, ``:216-220``).  With N GPUs each rank renders its row band
+into a packed [rows, W, 4] tile (``nerf_render_band``) and the tiles are gathered
+to rank 0 over RCCL (strong scaling: the frame is fixed).
 
 Rank 0 prints one JSON line.  ``roofline`` is the fine-MLP kernel's algorithmic
 FLOP rate (W*H_band*S*1,055,744 FLOP per launch, HIP events on the launch stream)
-against the dense MFMA peak of the compute dtype.  ``cpu_baseline`` times the
-oracle (a PyTorch-CPU restatement of the reference renderer) on a bounded row band
-of the same frame, on this node's host cores.
+against the dense MFMA peak of the compute dtype.  ``readme_grid`` times the
+reference README's resolution x samples grid for bf16, fp8 and fp32 with the same
+step (band + gather at N > 1), each cell with its fractions of the MFMA roofline.
+``cpu_baseline`` times the oracle (a PyTorch-CPU restatement of the reference
+renderer) on this node's host cores with the suite's protocol (2 views of
+``generate_test_poses(2)``), on bounded samples of three cells.
 """
 from __future__ import annotations
 
@@ -29,6 +33,8 @@ for _p in (REPO, os.path.join(REPO, "nerf-dbr_amd")):
 
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 METRIC = "rays/sec at 800x600x128spp (render_image, fine net, uniform samples)"
+GRID_RES = [(200, 150), (400, 300), (800, 600)]                 # reference main.py:134-141
+GRID_SPP = [32, 64, 128]
 
 
 def parse():
@@ -40,24 +46,93 @@ def parse():
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--spp", type=int, default=128)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="total CPU-baseline budget (0: skip)")
     ap.add_argument("--no-error-check", action="store_true", help="skip the bf16-vs-fp32 error band")
-    ap.add_argument("--no-extras", action="store_true", help="skip the other BASELINE configs (C2, C3, C5)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the other BASELINE configs and the grid")
+    ap.add_argument("--no-grid", action="store_true", help="skip the README resolution x spp grid")
     return ap.parse_args()
 
 
-def time_frames(render, n_warm, n_steps):
-    """Mean seconds per call of render() (device-synchronised)."""
+# ------------------------------------------------------------------ helpers --
+def sync_barrier(world):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def frame_step(r, pose, width, height, spp, rank, world):
+    """One frame of renderer r as the benchmark runs it: the whole frame at N = 1
+    (render_rows, the plugin's render_image path), else this rank's band rendered
+    into the packed tile and gathered to rank 0.  Returns (step, rays in this band)."""
     import torch
 
+    from nerf_amd import distributed as D
+
+    r0, r1 = D.band(rank, world, height)
+    if world == 1:
+        rgb = torch.empty(height, width, 3, device="cuda")
+        dep = torch.empty(height, width, device="cuda")
+        return (lambda: r.render_rows(pose, (width, height), spp, 0, height, rgb, dep)), width * height
+    tile = D.band_tile(world, height, width, r.torch_device())
+
+    def step():
+        r.render_band(pose, (width, height), spp, r0, r1, tile)
+        D.gather_tiles_to_root(tile, width, height)
+
+    return step, (r1 - r0) * width
+
+
+def time_steps(step, n_warm, n_steps, world):
+    """Max over ranks of the mean seconds per step (barrier + synchronize both sides)."""
+    from nerf_amd import distributed as D
+
     for _ in range(n_warm):
-        render()
-    torch.cuda.synchronize()
+        step()
+    sync_barrier(world)
     t0 = time.perf_counter()
     for _ in range(n_steps):
-        render()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / n_steps
+        step()
+    sync_barrier(world)
+    return D.reduce_max(time.perf_counter() - t0) / n_steps
+
+
+def kernel_ms(r, n, stage="fine_mlp"):
+    """Mean HIP-event time of a stage over the last n frames of renderer r."""
+    import numpy as np
+
+    return float(np.mean([f[stage] for f in r.hip.stage_ms_history(min(n, 64))]))
+
+
+# ------------------------------------------------------------ README grid --
+def readme_grid(renderers, pose, rank, world):
+    """rays/s on {200x150, 400x300, 800x600} x {32, 64, 128} spp for each precision,
+    with the fractions of the MFMA roofline: ``frac_frame`` = whole-job FLOP rate /
+    (N x peak), ``frac_kernel`` = the slowest rank's fine-MLP kernel rate / peak."""
+    from nerf_amd import distributed as D
+    from nerf_amd import weights as W
+
+    out = {}
+    for prec, r in renderers.items():
+        peak = PEAK_TFLOPS[prec]
+        rows = {}
+        for (w, h) in GRID_RES:
+            for spp in GRID_SPP:
+                step, band_rays = frame_step(r, pose, w, h, spp, rank, world)
+                n = 2 if prec == "fp32" and w * h * spp >= 400 * 300 * 128 else 4
+                dt = time_steps(step, 1, n, world)
+                kms = D.reduce_max(kernel_ms(r, n))
+                flop = w * h * spp * W.FLOPS_PER_SAMPLE
+                rows[f"{w}x{h}x{spp}"] = {
+                    "rays_per_s": w * h / dt, "ms_per_frame": 1e3 * dt,
+                    "frac_frame": flop / dt / 1e12 / (world * peak),
+                    "frac_kernel": band_rays * spp * W.FLOPS_PER_SAMPLE / (kms * 1e-3) / 1e12 / peak,
+                    "kernel_ms": kms}
+        out[prec] = rows
+    return out
 
 
 def other_configs(ckpt, pose, local, ref32):
@@ -68,13 +143,15 @@ def other_configs(ckpt, pose, local, ref32):
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
 
     out = {}
-    dt = time_frames(lambda: ref32.render_rows(pose, (400, 300), 64, 0, 300), 1, 3)
+    step, _ = frame_step(ref32, pose, 400, 300, 64, 0, 1)
+    dt = time_steps(step, 1, 3, 1)
     out["c2_fp32_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt}
 
     h = MI355XRenderer("bf16", n_importance=128, device_index=local)
     h.setup(ckpt)
     h.hip.set_profiling(True)
-    dt = time_frames(lambda: h.render_rows(pose, (800, 600), 64, 0, 600), 2, 5)
+    step, _ = frame_step(h, pose, 800, 600, 64, 0, 1)
+    dt = time_steps(step, 2, 5, 1)
     st = h.hip.stage_ms()
     flop = 800 * 600 * (64 + 192) * W.FLOPS_PER_SAMPLE
     mlp_ms = st["coarse_mlp"] + st["fine_mlp"]
@@ -86,8 +163,9 @@ def other_configs(ckpt, pose, local, ref32):
     f8 = MI355XRenderer("fp8", device_index=local)
     f8.setup(ckpt)
     f8.hip.set_profiling(True)
-    dt = time_frames(lambda: f8.render_rows(pose, (800, 600), 128, 0, 600), 2, 5)
-    ms = f8.hip.stage_ms()["fine_mlp"]
+    step, _ = frame_step(f8, pose, 800, 600, 128, 0, 1)
+    dt = time_steps(step, 2, 5, 1)
+    ms = kernel_ms(f8, 5)
     tf = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE / (ms * 1e-3) / 1e12
     rgb8, d8 = f8.render_rows(pose, (800, 600), 128, 292, 308)
     rgb32, d32 = ref32.render_rows(pose, (800, 600), 128, 292, 308)
@@ -97,72 +175,109 @@ def other_configs(ckpt, pose, local, ref32):
         "rgb_max_abs_vs_fp32": float((rgb8 - rgb32).abs().max()),
         "rgb_mean_abs_vs_fp32": float((rgb8 - rgb32).abs().mean()),
         "depth_max_abs_vs_fp32": float((d8 - d32).abs().max())}
-    return out
+    return out, f8
 
 
 def sharded_hierarchical(ckpt, pose, local, rank, world, width, height, n_warm=2, n_steps=5):
-    """C4: 64 coarse + 128 importance samples, bf16, each rank its row band, one
-    all-gather per frame; rays/s of the whole frame over the slowest rank."""
-    import torch
+    """C4: 64 coarse + 128 importance samples, bf16, each rank its row band rendered
+    into the packed tile, one gather to rank 0 per frame; rays/s of the whole frame
+    over the slowest rank."""
     import torch.distributed as dist
 
-    from nerf_amd import distributed as D
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
 
     h = MI355XRenderer("bf16", n_importance=128, device_index=local)
     h.setup(ckpt)
-    r0, r1 = D.band(rank, world, height)
-    rgb_b = torch.empty(r1 - r0, width, 3, device="cuda")
-    dep_b = torch.empty(r1 - r0, width, device="cuda")
-
-    def step():
-        h.render_rows(pose, (width, height), 64, r0, r1, rgb_b, dep_b)
-        D.gather_bands(rgb_b, dep_b, width, height)
-
-    for _ in range(n_warm):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(n_steps):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    dt = D.reduce_max(time.perf_counter() - t0) / n_steps
+    step, _ = frame_step(h, pose, width, height, 64, rank, world)
+    dt = time_steps(step, n_warm, n_steps, world)
     return {"rays_per_s": width * height / dt, "ms_per_frame": 1e3 * dt, "n_gpus": world,
             "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)",
-            "parallelism": f"row-band x{world} + {dist.get_backend()} all-gather"}
+            "parallelism": f"row-band x{world} + {dist.get_backend()} gather to rank 0"}
 
 
-def cpu_baseline(pose, width, height, spp, target_s):
-    """Oracle (PyTorch CPU) on a band of rows of the same frame; ~target_s seconds of CPU work."""
+# ------------------------------------------------------------- CPU baseline --
+def host_cpu_info():
+    """CPU model; logical CPUs of the machine and of this process's affinity mask;
+    physical cores behind that mask; the cgroup CPU quota, if any."""
+    info = {"model": "unknown CPU", "logical_machine": os.cpu_count()}
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["model"] = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    aff = sorted(os.sched_getaffinity(0))
+    info["logical_affinity"] = len(aff)
+    cores = set()
+    for c in aff:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            cores.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    info["physical_affinity"] = len(cores)
+    info["cgroup_quota_cpus"] = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def cpu_baseline(budget_s):
+    """The oracle's render_image on the host, the suite's protocol (wall clock around
+    render_image including ray generation, averaged over the 2 views of
+    generate_test_poses(2)), torch threads = physical cores in this process's
+    affinity mask (capped by the cgroup quota), 512-ray chunks.  Cells: 200x150x32
+    (whole frames), 400x300x64 and 800x600x128 (centre row bands sized to the budget).
+    The headline value is the 800x600x128 cell."""
+    import math
+
     import torch
 
     from nerf_amd import weights as W
+    from nerf_amd.benchmark.benchmark_suite import generate_test_poses
     from oracle import nerf_oracle as O
 
-    _, fine = W.synthetic_models(0)
-    net = O.Net(fine)
-    r0 = height // 2
-    t0 = time.time()
-    O.render_image(net, pose, (width, height), spp, rows=(r0, r0 + 2))
-    per_row = (time.time() - t0) / 2
-    rows = max(2, min(height - r0, int(target_s / max(per_row, 1e-6))))
-    t0 = time.time()
-    O.render_image(net, pose, (width, height), spp, rows=(r0, r0 + rows))
-    dt = time.time() - t0
-    cpu = "unknown CPU"
+    info = host_cpu_info()
+    threads = info["physical_affinity"]
+    if info["cgroup_quota_cpus"]:
+        threads = max(1, min(threads, int(math.floor(info["cgroup_quota_cpus"]))))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return {"value": rows * width / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle render_image rows [{r0},{r0 + rows}) of {width}x{height}x{spp} "
-                      f"({rows * width} rays, {dt:.1f} s, 512-ray chunks, torch {torch.__version__}, "
-                      f"{torch.get_num_threads()} threads on {cpu})"}
+        _, fine = W.synthetic_models(0)
+        net = O.Net(fine)
+        poses = generate_test_poses(2)
+
+        def rate(width, height, spp, rows):
+            r0 = (height - rows) // 2
+            t0 = time.perf_counter()
+            for p in poses:
+                O.render_image(net, p, (width, height), spp, rows=(r0, r0 + rows))
+            return rows * width * len(poses) / (time.perf_counter() - t0)
+
+        # calibrate each cell's rays/s on one row per view, then size its band
+        cells = {}
+        share = {"200x150x32": 0.2, "400x300x64": 0.3, "800x600x128": 0.5}
+        for key, (w, h, s) in (("200x150x32", (200, 150, 32)), ("400x300x64", (400, 300, 64)),
+                               ("800x600x128", (800, 600, 128))):
+            est = rate(w, h, s, 1)
+            rows = int(min(h, max(2, share[key] * budget_s * est / (2 * w))))
+            v = rate(w, h, s, rows)
+            cells[key] = {"rays_per_s": v, "rows": rows, "rays_timed": 2 * rows * w}
+    finally:
+        torch.set_num_threads(prev)
+    head = cells["800x600x128"]
+    return {"value": head["rays_per_s"], "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle render_image (PyTorch-CPU restatement of PyTorchCPURenderer, 512-ray chunks), "
+                       f"2 views of generate_test_poses(2), centre band of {head['rows']} rows of 800x600x128 "
+                       f"per view ({head['rays_timed']} rays), {threads} torch threads, torch {torch.__version__}"),
+            "threads": threads, "host": info, "cells": cells}
 
 
+# --------------------------------------------------------------------- main --
 def main():
     args = parse()
     # stdout carries exactly one JSON line; the renderers' reference-style
@@ -191,39 +306,23 @@ def main():
 
     pose = torch.eye(4)            # benchmark_suite.generate_test_poses view 0
     pose[2, 3] = 4.0
-    r0, r1 = D.band(rank, world, height)
-    band_rays = (r1 - r0) * width
-    rgb_b = torch.empty(r1 - r0, width, 3, device="cuda")
-    dep_b = torch.empty(r1 - r0, width, device="cuda")
-
-    def step():
-        r.render_rows(pose, (width, height), spp, r0, r1, rgb_b, dep_b)
-        if world > 1:
-            D.gather_bands(rgb_b, dep_b, width, height)
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+    step, band_rays = frame_step(r, pose, width, height, spp, rank, world)
 
     for _ in range(args.warmup):
         step()
-    barrier()
+    sync_barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()                                          # queued back to back: no host sync per frame
-    barrier()
+    sync_barrier(world)
     elapsed = D.reduce_max(time.perf_counter() - t0)   # max over ranks
     # the fine-MLP kernel's HIP-event times of the timed frames (the library's
     # per-frame event ring, recorded on the launch stream)
-    n_hist = min(args.steps, 64)
-    mlp_ms = [f["fine_mlp"] for f in r.hip.stage_ms_history(n_hist)]
+    kern_ms = kernel_ms(r, args.steps)
     ms_step = 1000.0 * elapsed / args.steps
     value = width * height * args.steps / elapsed
 
     flop_launch = band_rays * spp * W.FLOPS_PER_SAMPLE
-    kern_ms = float(np.mean(mlp_ms))
     traffic, traffic_src = None, None
     kname = f"mlp_{args.precision}_kernel"
     pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
@@ -241,21 +340,24 @@ def main():
     extra = {}
     if world > 1 and not args.no_extras:
         # BASELINE config 4: the 64+128 hierarchical frame (bf16), sharded in row
-        # bands over every rank and all-gathered -- every rank takes part
+        # bands over every rank and gathered to rank 0 -- every rank takes part
         extra["c4_hierarchical_sharded"] = sharded_hierarchical(ckpt, pose, local, rank, world, width, height)
         # per-frame breakdown at N GPUs: the slowest rank's MLP kernel
-        # and the exchange alone (the step's packing copies + all-gather), 10 frames
-        barrier()
+        # and the exchange alone (the gather of the packed tiles), 10 frames
+        tile = D.band_tile(world, height, width, r.torch_device())
+        sync_barrier(world)
         t_x = time.perf_counter()
         for _ in range(10):
-            D.gather_bands(rgb_b, dep_b, width, height)
-        barrier()
+            D.gather_tiles_to_root(tile, width, height)
+        sync_barrier(world)
         extra["exchange_ms_per_frame"] = 1e3 * D.reduce_max(time.perf_counter() - t_x) / 10
         extra["mlp_ms_per_frame_rank_max"] = D.reduce_max(kern_ms)
-    ref = None
-    if rank == 0 and ((args.precision != "fp32" and not args.no_error_check) or (world == 1 and not args.no_extras)):
-        ref = MI355XRenderer("fp32", device_index=local)
-        ref.setup(ckpt)
+    ref = f8 = None
+    if (args.precision != "fp32" and not args.no_error_check and rank == 0) or not args.no_extras:
+        ref = r if args.precision == "fp32" else MI355XRenderer("fp32", device_index=local)
+        if ref is not r:
+            ref.setup(ckpt)
+        ref.hip.set_profiling(True)
     if rank == 0 and args.precision != "fp32" and not args.no_error_check:
         # bf16 / fp8 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
         a0, a1 = height // 2 - 8, height // 2 + 8
@@ -264,18 +366,26 @@ def main():
         extra[f"{args.precision}_vs_fp32_rgb_max_abs"] = float((rgb_lp - rgb32).abs().max())
         extra[f"{args.precision}_vs_fp32_rgb_mean_abs"] = float((rgb_lp - rgb32).abs().mean())
         extra[f"{args.precision}_vs_fp32_depth_max_abs"] = float((d_lp - d32).abs().max())
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        ref.render_rows(pose, (width, height), spp, 0, height)
-        torch.cuda.synchronize()
-        extra["fp32_path_rays_per_s_1gpu"] = width * height / (time.perf_counter() - t1)
 
-    if rank == 0 and world == 1 and not args.no_extras:
-        extra["other_configs"] = other_configs(ckpt, pose, local, ref)
+    if world == 1 and not args.no_extras:
+        extra["other_configs"], f8 = other_configs(ckpt, pose, local, ref)
+    if not args.no_extras and not args.no_grid:
+        # every rank takes part (bands + gather at N > 1)
+        if f8 is None:
+            f8 = r if args.precision == "fp8" else MI355XRenderer("fp8", device_index=local)
+            if f8 is not r:
+                f8.setup(ckpt)
+        f8.hip.set_profiling(True)
+        rs = {"bf16": r if args.precision == "bf16" else None, "fp8": f8, "fp32": ref}
+        if rs["bf16"] is None:
+            rs["bf16"] = MI355XRenderer("bf16", device_index=local)
+            rs["bf16"].setup(ckpt)
+            rs["bf16"].hip.set_profiling(True)
+        extra["readme_grid"] = readme_grid(rs, pose, rank, world)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(pose, width, height, spp, args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds)
 
     if rank == 0:
         out = {
@@ -294,8 +404,8 @@ def main():
             "config": {"workload": f"render_image {width}x{height}, {spp} uniform samples/ray, fine net",
                        "resolution": [width, height], "samples_per_ray": spp,
                        "parallelism": (f"row-band x{world} + "
-                                       f"{'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all-gather"
-                                       if world > 1 else "1 GPU")},
+                                       f"{'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
+                                       f"gather to rank 0" if world > 1 else "1 GPU")},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_ms,

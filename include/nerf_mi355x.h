@@ -9,8 +9,10 @@
  *
  * Device pointers are HIP device memory on the context's device; `stream` is a
  * hipStream_t (NULL = the legacy default stream).  Calls on one context are
- * serialised on the caller's stream; the context owns its packed weights and
- * its scratch, the caller owns every input/output buffer.
+ * serialised on the caller's stream; a render issued on a different stream than
+ * the previous render waits (on the device) for that render to finish, since
+ * both use the context's scratch.  The context owns its packed weights and its
+ * scratch, the caller owns every input/output buffer.
  *
  * Each entry point names the reference interface it replaces
  * (paths relative to dgsmith7/nerf-dbr).
@@ -147,6 +149,29 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
                         float focal, float near_, float far_, const float* t_vals, int n_samples,
                         int n_importance, const float* u, const float* t_rand, const float* u_rays,
                         int precision, float* rgb_out, float* depth_out, void* stream);
+
+/* Replaces: PyTorchCPURenderer.render_image (src/benchmark/pytorch_renderers.py:127-154) for one
+ * row band [row0, row1) of the frame, written as the packed tile the multi-GPU gather moves
+ * (SURVEY §8e): rgbd_out device [(row1-row0)*width][4] = (r, g, b, depth).  Otherwise as
+ * nerf_render. */
+int nerf_render_band(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1,
+                     float focal, float near_, float far_, const float* t_vals, int n_samples,
+                     int n_importance, const float* u, int precision, float* rgbd_out, void* stream);
+
+/* The fine-pass sample depths of the last hierarchical render on this context: the sorted
+ * union of coarse and importance samples (the z_samples VolumeRenderer.importance_sample
+ * returns, src/utils/rendering.py:54-100, merged with the coarse z), device
+ * [n_rays][per_ray].  n_rays / per_ray must match that render; NERF_E_INVALID otherwise.
+ * The copy is queued on `stream`. */
+int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, void* stream);
+
+/* Replaces: PositionalEncoding.encode (src/models/nerf.py:31-45) for the model's two
+ * encodings (n_freqs 10: positions, 4: directions): x device [n][3] -> out device
+ * [n][3 + 6*n_freqs] = [x, sin(2^0 pi x), cos(2^0 pi x), sin(2^1 pi x), ...] -- the values
+ * the MLP kernels of `precision` compute before rounding them to the MFMA's input type.
+ * NERF_FP32: accurate sincosf of fl(2^k*pi)*x (the parity path); NERF_BF16 / NERF_FP8: one
+ * reduced sin/cos per coordinate and lane half, then angle doubling (nerf_device.h). */
+int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream);
 
 /* Replaces: BaseUnifiedRenderer.sample_points_on_rays (src/benchmark/base_renderer.py:260-281)
  * and, with t_rand, VolumeRenderer.sample_points_on_rays(perturb=True)

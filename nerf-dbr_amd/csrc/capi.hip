@@ -69,6 +69,13 @@ struct nerf_ctx {
   const float* up_zbuf = nullptr;
   const float* up_wbuf = nullptr;
   hipEvent_t stage_ev = nullptr; // recorded after the last upload from host_stage
+  // The stream of the last render: a render on another stream first waits for the
+  // previous render's end event (its uploads and its use of the shared scratch)
+  hipStream_t last_stream = nullptr;
+  // the fine-pass sample depths of the last hierarchical render (nerf_ctx_last_fine_z)
+  const float* last_zfine = nullptr;
+  long last_zfine_rays = 0;
+  int last_zfine_per_ray = 0;
   bool profiling = false;
   int fused_composite = 3;     // NERF_OPT_FUSED_COMPOSITE bits: 1 render passes, 2 hierarchical coarse pass
   // stage events of the last kEvFrames renders (a ring, so that per-frame stage
@@ -339,10 +346,16 @@ int nerf_render(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
                              u, nullptr, nullptr, precision, rgb_out, depth_out, stream);
 }
 
-int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal,
-                        float near_, float far_, const float* t_vals, int n_samples, int n_importance, const float* u,
-                        const float* t_rand, const float* u_rays, int precision, float* rgb_out, float* depth_out,
-                        void* stream) {
+}  // extern "C"
+
+namespace {
+
+// The whole render path (nerf_render, nerf_render_sampled, nerf_render_band):
+// outputs at rgb_out + os.rgb * ray and depth_out + os.depth * ray.
+int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal,
+                float near_, float far_, const float* t_vals, int n_samples, int n_importance, const float* u,
+                const float* t_rand, const float* u_rays, int precision, float* rgb_out, float* depth_out,
+                OutStrides os, void* stream) {
   const int net_main = NERF_NET_FINE;
   int rc = check_net(ctx, net_main, precision);
   if (rc != NERF_OK) return rc;
@@ -360,6 +373,11 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   if (n_rays * n_fine > 0x7FFFFFFFL * 128L) return set_error(NERF_E_INVALID, "nerf_render: too many samples");
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
+  if (ctx->n_frames > 0 && s != ctx->last_stream) {
+    // another stream than the last render's: order this render after that one
+    // (the uploads it skips below and the scratch buffers are shared)
+    HIP_TRY(hipStreamWaitEvent(s, ctx->frames[(ctx->n_frames - 1) % nerf_ctx::kEvFrames].ev[NERF_N_STAGES], 0));
+  }
 
   // z table (base_renderer.py:274-275) and the importance draw
   std::vector<float> hz(n_samples), hu(n_importance);
@@ -376,7 +394,10 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   if ((rc = grow(ctx->zbuf, ctx->z_cap, zfloats, "z")) != NERF_OK) return rc;
   const size_t wfloats = 1024 + (n_importance > 0 ? size_t(n_rays) * n_samples : 0);
   if ((rc = grow(ctx->wbuf, ctx->w_cap, wfloats, "weights")) != NERF_OK) return rc;
-  if (ctx->z_cap != z_cap0) ctx->up_zbuf = nullptr;   // reallocated: the uploaded tables are gone
+  if (ctx->z_cap != z_cap0) {   // reallocated: the uploaded tables (and the last fine z) are gone
+    ctx->up_zbuf = nullptr;
+    ctx->last_zfine = nullptr;
+  }
   if (ctx->w_cap != w_cap0) ctx->up_wbuf = nullptr;
 
   float* d_ztab = ctx->zbuf;
@@ -442,13 +463,16 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
     if ((rc = mark(2)) != NERF_OK) return rc;
     if (!fuse_coarse)
       HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_first, z_first_stride, rays_d, int(n_rays),
-                               n_samples, rgb_out, depth_out, nullptr, d_w, s));
+                               n_samples, rgb_out, depth_out, nullptr, d_w, s, os));
     HIP_TRY(launch_importance(z_first, z_first_stride, d_w, u_rays ? u_rays : d_u, u_rays ? n_importance : 0,
                               int(n_rays), n_samples, n_importance, d_zfine, s,
                               fuse_coarse ? ctx->mlp_out : nullptr));
     fr.ran[2] = true;
     z_main = d_zfine;
     z_stride = n_fine;
+    ctx->last_zfine = d_zfine;
+    ctx->last_zfine_rays = n_rays;
+    ctx->last_zfine_per_ray = n_fine;
   } else {
     if ((rc = mark(2)) != NERF_OK) return rc;
   }
@@ -465,13 +489,59 @@ int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, 
   }
   if ((rc = mark(4)) != NERF_OK) return rc;
   if (fused)
-    HIP_TRY(launch_composite_segments(ctx->mlp_out, int(n_rays), n_fine / 32, rgb_out, depth_out, s));
+    HIP_TRY(launch_composite_segments(ctx->mlp_out, int(n_rays), n_fine / 32, rgb_out, depth_out, s, os));
   else
     HIP_TRY(launch_composite(ctx->mlp_out, 4, ctx->mlp_out + 1, 4, z_main, z_stride, rays_d, int(n_rays), n_fine,
-                             rgb_out, depth_out, nullptr, nullptr, s));
+                             rgb_out, depth_out, nullptr, nullptr, s, os));
   fr.ran[4] = true;
   HIP_TRY(hipEventRecord(fr.ev[NERF_N_STAGES], s));
   ++ctx->n_frames;
+  ctx->last_stream = s;
+  return NERF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nerf_render_sampled(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal,
+                        float near_, float far_, const float* t_vals, int n_samples, int n_importance, const float* u,
+                        const float* t_rand, const float* u_rays, int precision, float* rgb_out, float* depth_out,
+                        void* stream) {
+  return render_impl(ctx, c2w, width, height, row0, row1, focal, near_, far_, t_vals, n_samples, n_importance, u,
+                     t_rand, u_rays, precision, rgb_out, depth_out, OutStrides{}, stream);
+}
+
+int nerf_render_band(nerf_ctx* ctx, const float* c2w, int width, int height, int row0, int row1, float focal,
+                     float near_, float far_, const float* t_vals, int n_samples, int n_importance, const float* u,
+                     int precision, float* rgbd_out, void* stream) {
+  if (row1 > row0 && !rgbd_out) return set_error(NERF_E_INVALID, "nerf_render_band: null output");
+  return render_impl(ctx, c2w, width, height, row0, row1, focal, near_, far_, t_vals, n_samples, n_importance, u,
+                     nullptr, nullptr, precision, rgbd_out, rgbd_out ? rgbd_out + 3 : nullptr, OutStrides{4, 4},
+                     stream);
+}
+
+int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, void* stream) {
+  if (!ctx || !z_out) return set_error(NERF_E_INVALID, "nerf_ctx_last_fine_z: null argument");
+  if (!ctx->last_zfine) return set_error(NERF_E_INVALID, "nerf_ctx_last_fine_z: no hierarchical render yet");
+  if (n_rays != ctx->last_zfine_rays || per_ray != ctx->last_zfine_per_ray)
+    return set_error(NERF_E_INVALID, "nerf_ctx_last_fine_z: the last hierarchical render had %ld rays x %d samples",
+                     ctx->last_zfine_rays, ctx->last_zfine_per_ray);
+  DeviceGuard g(ctx->device);
+  HIP_TRY(hipMemcpyAsync(z_out, ctx->last_zfine, sizeof(float) * size_t(n_rays) * per_ray, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return NERF_OK;
+}
+
+int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream) {
+  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8)
+    return set_error(NERF_E_INVALID, "bad precision %d", precision);
+  if (n < 0 || (n_freqs != kPosL && n_freqs != kDirL))
+    return set_error(NERF_E_INVALID, "nerf_positional_encoding: n %ld, n_freqs %d (the model's are 10 and 4)", n,
+                     n_freqs);
+  if (n == 0) return NERF_OK;
+  if (!x || !out) return set_error(NERF_E_INVALID, "nerf_positional_encoding: null pointer");
+  HIP_TRY(launch_encode(x, n, n_freqs, precision != NERF_FP32, out, (hipStream_t)stream));
   return NERF_OK;
 }
 

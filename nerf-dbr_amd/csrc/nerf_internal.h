@@ -11,6 +11,13 @@ namespace nerf {
 
 struct SampleSrc;
 
+// Element strides of a render's per-ray outputs: rgb at rgb*r (3: [R][3]; 4: the
+// packed [R][4] band of nerf_render_band, depth then at offset 3), depth at depth*r.
+struct OutStrides {
+  int rgb = 3;
+  int depth = 1;
+};
+
 // Compute units of the current device (cached per device): the grid of the
 // persistent MLP kernels, one workgroup per CU.
 int current_device_cus();
@@ -30,11 +37,15 @@ hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc
                           float* wloc = nullptr);
 // Chains each ray's segment records into (rgb, depth) (nerf_device.h SegRecord).
 hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
-                                     hipStream_t stream);
+                                     hipStream_t stream, OutStrides os = {});
 hipError_t launch_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride,
                             const float* z, int z_ray_stride, const float* rays_d, int n_rays, int n_samples,
                             float* rgb_out, float* depth_out, float* acc_out, float* weights_out,
-                            hipStream_t stream);
+                            hipStream_t stream, OutStrides os = {});
+// PositionalEncoding.encode (nerf.py:31-45) as the MLP kernels evaluate it:
+// x [n][3] -> out [n][3 + 6*n_freqs] in the reference's channel order; fast =
+// the bf16/fp8 kernels' reduced sin/cos with angle doubling, else accurate sincosf.
+hipError_t launch_encode(const float* x, long n, int n_freqs, bool fast, float* out, hipStream_t stream);
 hipError_t launch_sample(const float* z_tab, const float* t_rand, int n_rays, int n_samples, const float* rays_o,
                          const float* rays_d, float* z_out, float* points_out, hipStream_t stream);
 // seg (optional): weights are in-segment weights of a fused coarse pass, scaled

@@ -41,7 +41,7 @@ __global__ void rays_kernel(Pose pose, int width, float half_w, float half_h, fl
 __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stride, const float* __restrict__ rgb,
                                  int rgb_stride, const float* __restrict__ z, int z_ray_stride,
                                  const float* __restrict__ rays_d, int n_rays, int n_samples,
-                                 float* __restrict__ rgb_out, float* __restrict__ depth_out,
+                                 float* __restrict__ rgb_out, float* __restrict__ depth_out, OutStrides os,
                                  float* __restrict__ acc_out, float* __restrict__ weights_out) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
@@ -50,8 +50,9 @@ __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stri
     // `dists[..., :1]` of the empty difference tensor is empty, so every
     // per-sample array is empty and the image is all zeros
     // (pytorch_renderers.py:107-108; same in rendering.py:105-106).
-    rgb_out[3L * r] = rgb_out[3L * r + 1] = rgb_out[3L * r + 2] = 0.0f;
-    depth_out[r] = 0.0f;
+    float* o = rgb_out + long(os.rgb) * r;
+    o[0] = o[1] = o[2] = 0.0f;
+    depth_out[long(os.depth) * r] = 0.0f;
     if (acc_out) acc_out[r] = 0.0f;
     return;
   }
@@ -78,10 +79,11 @@ __global__ void composite_kernel(const float* __restrict__ sigma, int sigma_stri
     T_acc = __dmul_rn(T_acc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
     z_cur = z_next;
   }
-  rgb_out[3L * r] = cr;
-  rgb_out[3L * r + 1] = cg;
-  rgb_out[3L * r + 2] = cb;
-  depth_out[r] = dep;
+  float* o = rgb_out + long(os.rgb) * r;
+  o[0] = cr;
+  o[1] = cg;
+  o[2] = cb;
+  depth_out[long(os.depth) * r] = dep;
   if (acc_out) acc_out[r] = acc;
 }
 
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(64 * kImpWaves) void importance_wave_kernel(
 // samples at a time (whole cache lines per request).
 __global__ void composite_packed_kernel(const f32x4* __restrict__ mlp, const float* __restrict__ z, int z_ray_stride,
                                         const float* __restrict__ rays_d, int n_rays, int n_samples,
-                                        float* __restrict__ rgb_out, float* __restrict__ depth_out,
+                                        float* __restrict__ rgb_out, float* __restrict__ depth_out, OutStrides os,
                                         float* __restrict__ acc_out, float* __restrict__ weights_out) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
@@ -329,10 +331,11 @@ __global__ void composite_packed_kernel(const f32x4* __restrict__ mlp, const flo
       T_acc = __dmul_rn(T_acc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
     }
   }
-  rgb_out[3L * r] = cr;
-  rgb_out[3L * r + 1] = cg;
-  rgb_out[3L * r + 2] = cb;
-  depth_out[r] = dep;
+  float* o = rgb_out + long(os.rgb) * r;
+  o[0] = cr;
+  o[1] = cg;
+  o[2] = cb;
+  depth_out[long(os.depth) * r] = dep;
   if (acc_out) acc_out[r] = acc;
 }
 
@@ -341,7 +344,7 @@ __global__ void composite_packed_kernel(const f32x4* __restrict__ mlp, const flo
 //   rgb += float(T) * rgb_k, depth += float(T) * depth_k, T *= P_k (double),
 // the regrouped form of composite_kernel's sequential sums.  One thread per ray.
 __global__ void composite_segments_kernel(const SegRecord* __restrict__ seg, int n_rays, int n_segments,
-                                          float* __restrict__ rgb_out, float* __restrict__ depth_out) {
+                                          float* __restrict__ rgb_out, float* __restrict__ depth_out, OutStrides os) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
   const SegRecord* sr = seg + long(r) * n_segments;
@@ -356,10 +359,11 @@ __global__ void composite_segments_kernel(const SegRecord* __restrict__ seg, int
     dep = __fadd_rn(dep, __fmul_rn(t, rec.depth));
     T = __dmul_rn(T, rec.P);
   }
-  rgb_out[3L * r] = cr;
-  rgb_out[3L * r + 1] = cg;
-  rgb_out[3L * r + 2] = cb;
-  depth_out[r] = dep;
+  float* o = rgb_out + long(os.rgb) * r;
+  o[0] = cr;
+  o[1] = cg;
+  o[2] = cb;
+  depth_out[long(os.depth) * r] = dep;
 }
 
 // Sample depths and points, one thread per (ray, sample).
@@ -390,6 +394,37 @@ __global__ void sample_kernel(const float* __restrict__ z_tab, const float* __re
   }
 }
 
+// PositionalEncoding.encode (nerf.py:31-45) through the MLP kernels' own device
+// code (nerf_device.h pos_encode / dir_encode): one thread per (sample, lane
+// half h), each half writing the features its slots own (pe_slot_feature /
+// dpe_slot_feature), so the result is exactly what the kernels feed the MFMAs
+// before rounding to bf16 / e4m3.
+template <bool kFast, bool kPos>
+__global__ void encode_kernel(const float* __restrict__ x, long n, float* __restrict__ out) {
+  const long i = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= 2 * n) return;
+  const long p = i >> 1;
+  const int h = int(i & 1);
+  const float x0 = x[3 * p], x1 = x[3 * p + 1], x2 = x[3 * p + 2];
+  if (kPos) {
+    float pe[32];
+    pos_encode<kFast>(x0, x1, x2, h, pe);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int f = pe_slot_feature(h, q);
+      if (f >= 0) out[p * kPosDim + f] = pe[q];
+    }
+  } else {
+    float de[16];
+    dir_encode<kFast>(x0, x1, x2, h, de);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int f = dpe_slot_feature(h, q);
+      if (f >= 0) out[p * kDirDim + f] = de[q];
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_sample(const float* z_tab, const float* t_rand, int n_rays, int n_samples, const float* rays_o,
@@ -400,6 +435,22 @@ hipError_t launch_sample(const float* z_tab, const float* t_rand, int n_rays, in
   const dim3 grid{unsigned((n + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
   hipLaunchKernelGGL(sample_kernel, grid, block, 0, stream, z_tab, t_rand, n_samples, n, rays_o, rays_d, z_out,
                      points_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode(const float* x, long n, int n_freqs, bool fast, float* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int threads = 256;
+  const dim3 grid{unsigned((2 * n + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
+  if (n_freqs == kPosL) {
+    if (fast) hipLaunchKernelGGL((encode_kernel<true, true>), grid, block, 0, stream, x, n, out);
+    else hipLaunchKernelGGL((encode_kernel<false, true>), grid, block, 0, stream, x, n, out);
+  } else if (n_freqs == kDirL) {
+    if (fast) hipLaunchKernelGGL((encode_kernel<true, false>), grid, block, 0, stream, x, n, out);
+    else hipLaunchKernelGGL((encode_kernel<false, false>), grid, block, 0, stream, x, n, out);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -422,28 +473,28 @@ hipError_t launch_generate_rays(const float* c2w, int width, int height, int row
 
 hipError_t launch_composite(const float* sigma, int sigma_stride, const float* rgb, int rgb_stride, const float* z,
                             int z_ray_stride, const float* rays_d, int n_rays, int n_samples, float* rgb_out,
-                            float* depth_out, float* acc_out, float* weights_out, hipStream_t stream) {
+                            float* depth_out, float* acc_out, float* weights_out, hipStream_t stream, OutStrides os) {
   if (n_rays <= 0) return hipSuccess;
   const int threads = 128;
   const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
   if (sigma_stride == 4 && rgb_stride == 4 && rgb == sigma + 1 && n_samples > 1 &&
       (reinterpret_cast<uintptr_t>(sigma) & 15) == 0) {
     hipLaunchKernelGGL(composite_packed_kernel, grid, block, 0, stream, (const f32x4*)sigma, z, z_ray_stride, rays_d,
-                       n_rays, n_samples, rgb_out, depth_out, acc_out, weights_out);
+                       n_rays, n_samples, rgb_out, depth_out, os, acc_out, weights_out);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(composite_kernel, grid, block, 0, stream, sigma, sigma_stride, rgb, rgb_stride, z, z_ray_stride,
-                     rays_d, n_rays, n_samples, rgb_out, depth_out, acc_out, weights_out);
+                     rays_d, n_rays, n_samples, rgb_out, depth_out, os, acc_out, weights_out);
   return hipGetLastError();
 }
 
 hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
-                                     hipStream_t stream) {
+                                     hipStream_t stream, OutStrides os) {
   if (n_rays <= 0) return hipSuccess;
   const int threads = 256;
   const dim3 grid{unsigned((n_rays + threads - 1) / threads), 1, 1}, block{threads, 1, 1};
   hipLaunchKernelGGL(composite_segments_kernel, grid, block, 0, stream, (const SegRecord*)seg, n_rays, n_segments,
-                     rgb_out, depth_out);
+                     rgb_out, depth_out, os);
   return hipGetLastError();
 }
 

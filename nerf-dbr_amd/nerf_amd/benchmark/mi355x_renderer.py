@@ -121,6 +121,28 @@ class MI355XRenderer(BaseUnifiedRenderer):
                             rgb_out, depth_out, t_rand=tr, u_rays=ur)
         return rgb_out, depth_out
 
+    def torch_device(self):
+        import torch
+
+        return torch.device("cuda", self.device_index)
+
+    def render_band(self, camera_pose, resolution: Tuple[int, int], samples_per_ray: int, row0: int, row1: int,
+                    out=None):
+        """Rows [row0, row1) as one packed device tensor [rows, W, 4] = (r, g, b, depth)
+        (nerf_render_band): the tile the multi-GPU gather moves, written in place."""
+        import torch
+
+        width, height = resolution
+        rows = row1 - row0
+        if out is None:
+            out = torch.empty(rows, width, 4, dtype=torch.float32, device=self.torch_device())
+        u_shared = self._u(self.n_importance) if self.n_importance else None
+        with torch.cuda.device(self.device_index):
+            self.hip.render_band(_pose_np(camera_pose), width, height, row0, row1, self.focal, self.near, self.far,
+                                 t_vals(samples_per_ray), self.n_importance, u_shared,
+                                 rt.PRECISIONS[self.precision], out)
+        return out
+
     def render_image(self, camera_pose, resolution: Tuple[int, int], samples_per_ray: int = 64):
         """PyTorchCPURenderer.render_image semantics (pytorch_renderers.py:127-154)."""
         width, height = resolution

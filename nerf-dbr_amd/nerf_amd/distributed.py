@@ -2,11 +2,14 @@
 
 Rays are independent and cost the same (fixed samples per ray), so the frame
 is cut into contiguous row bands, rank r rendering rows
-``[floor(r*H/P), floor((r+1)*H/P))``.  The only exchange is one
-all-gather of the bands' packed ``[rows, W, 4]`` fp32 (RGB + depth) over
-RCCL/xGMI (backend "nccl" on ROCm) -- 960 KB per rank at 800x600 on 8 GPUs.
-The reference has no distributed path at all; this replaces nothing and adds
-the multi-GPU mode the benchmark reports.
+``[floor(r*H/P), floor((r+1)*H/P))``.  Each rank renders its band
+straight into a packed ``[rows, W, 4]`` fp32 tile (RGB + depth,
+``nerf_render_band``), and the only exchange is one gather of those tiles to
+the root over RCCL/xGMI (backend "nccl" on ROCm): 960 KB per rank at 800x600 on
+8 GPUs, each rank's tile on its own direct xGMI link to the root.  An
+all-gather (every rank receives the frame) is kept as an option.  The reference
+has no distributed path at all; this replaces nothing and adds the multi-GPU
+mode the benchmark reports.
 """
 from __future__ import annotations
 
@@ -40,8 +43,52 @@ def _gather_buffers(world: int, rows: int, width: int, device):
     return _GATHER_BUFS[key]
 
 
+def band_tile(world: int, height: int, width: int, device):
+    """The cached packed send tile of this shape ([max band rows, W, 4]); a rank
+    renders its band into its first rows (nerf_render_band)."""
+    rows = max_band_rows(world, height)
+    key = ("tile", world, rows, width, str(device))
+    if key not in _GATHER_BUFS:
+        import torch
+
+        _GATHER_BUFS[key] = torch.zeros(rows, width, 4, dtype=torch.float32, device=device)
+    return _GATHER_BUFS[key]
+
+
+def gather_tiles_to_root(tile, width: int, height: int, root: int = 0, group=None):
+    """Gather every rank's packed band tile ([max rows, W, 4]) to `root`: one
+    ``dist.gather`` (RCCL: the root receives from each rank on its own xGMI link).
+    Returns the frame as a packed [H, W, 4] tensor on the root (its views
+    [..., :3] and [..., 3] are the RGB and depth images), None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    rows = tile.shape[0]
+    key = ("full", world, rows, width, str(tile.device))
+    if key not in _GATHER_BUFS:
+        _GATHER_BUFS[key] = torch.empty(world, rows, width, 4, dtype=torch.float32, device=tile.device)
+    full = _GATHER_BUFS[key]
+    if tile.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal of the multi-rank path on one device (gloo gathers host tensors)
+        host = [torch.empty(rows, width, 4) for _ in range(world)] if rank == root else None
+        dist.gather(tile.cpu(), host, dst=root, group=group)
+        if rank == root:
+            for r in range(world):
+                full[r].copy_(host[r])
+    else:
+        dist.gather(tile, list(full.unbind(0)) if rank == root else None, dst=root, group=group)
+    if rank != root:
+        return None
+    if height % world == 0:
+        return full.reshape(world * rows, width, 4)
+    return torch.cat([full[r, : b1 - b0] for r, (b0, b1) in enumerate(bands(world, height))], 0)
+
+
 def gather_bands(rgb_band, depth_band, width: int, height: int, group=None):
-    """All-gather every rank's band into the full (rgb [H,W,3], depth [H,W]) on every rank.
+    """All-gather every rank's band into the full (rgb [H,W,3], depth [H,W]) on every rank
+    (the option beside gather_tiles_to_root; it packs the separate rgb/depth bands first).
 
     Bands are padded to the largest band so one ``all_gather_into_tensor`` moves them
     (with H divisible by the world size, as 600 rows over 1/2/4/8 GPUs, there is no
@@ -108,6 +155,22 @@ def reduce_max(x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def render_frame_to_root(renderer, camera_pose, resolution: Tuple[int, int], samples_per_ray: int,
+                         root: int = 0, group=None):
+    """This rank renders its band into the packed tile (renderer.render_band) and the
+    tiles are gathered to `root`: (rgb [H,W,3], depth [H,W]) views on the root, None elsewhere."""
+    import torch.distributed as dist
+
+    width, height = resolution
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    r0, r1 = band(rank, world, height)
+    tile = band_tile(world, height, width, renderer.torch_device())
+    renderer.render_band(camera_pose, resolution, samples_per_ray, r0, r1, tile)
+    full = gather_tiles_to_root(tile, width, height, root, group)
+    return None if full is None else (full[..., :3], full[..., 3])
 
 
 def render_sharded(render_rows: Callable, camera_pose, resolution: Tuple[int, int], samples_per_ray: int,

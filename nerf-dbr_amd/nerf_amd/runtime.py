@@ -66,6 +66,10 @@ SIGNATURES = {
     "nerf_ctx_stage_ms": (_c.c_int, [_P, _FP]),
     "nerf_ctx_set_option": (_c.c_int, [_P, _c.c_int, _c.c_int]),
     "nerf_ctx_stage_ms_history": (_c.c_int, [_P, _c.c_int, _FP]),
+    "nerf_render_band": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float,
+                                    _c.c_float, _FP, _c.c_int, _c.c_int, _FP, _c.c_int, _P, _P]),
+    "nerf_ctx_last_fine_z": (_c.c_int, [_P, _c.c_long, _c.c_int, _P, _P]),
+    "nerf_positional_encoding": (_c.c_int, [_c.c_int, _P, _c.c_long, _c.c_int, _P, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -258,6 +262,26 @@ class Device:
                                             _ptr(t_rand), _ptr(u_rays), precision, _ptr(rgb_out), _ptr(depth_out),
                                             _stream(stream)))
 
+    def render_band(self, c2w: np.ndarray, width: int, height: int, row0: int, row1: int, focal: float,
+                    near: float, far: float, t_vals: np.ndarray, n_importance: int, u: Optional[np.ndarray],
+                    precision: int, rgbd_out, stream=None) -> None:
+        """Rows [row0, row1) into the packed [rows, W, 4] (r, g, b, depth) device tensor rgbd_out."""
+        pose = np.ascontiguousarray(np.asarray(c2w, dtype=np.float32).reshape(4, 4))
+        t = np.ascontiguousarray(t_vals, dtype=np.float32)
+        uu = None if u is None else np.ascontiguousarray(u, dtype=np.float32)
+        n = (row1 - row0) * width
+        if rgbd_out.numel() < 4 * n or not rgbd_out.is_contiguous() or rgbd_out.dtype != torch_float32():
+            raise ValueError(f"rgbd_out must be a contiguous float32 tensor of >= {4 * n} elements")
+        _check(self.lib.nerf_render_band(self._ctx, _fptr(pose), width, height, row0, row1, focal, near, far,
+                                         _fptr(t), t.size, n_importance, None if uu is None else _fptr(uu),
+                                         precision, _ptr(rgbd_out), _stream(stream)))
+
+    def last_fine_z(self, n_rays: int, per_ray: int, out, stream=None) -> None:
+        """The last hierarchical render's fine-pass sample depths [n_rays, per_ray] into out."""
+        if out.numel() < n_rays * per_ray or not out.is_contiguous():
+            raise ValueError("out too small or not contiguous")
+        _check(self.lib.nerf_ctx_last_fine_z(self._ctx, n_rays, per_ray, _ptr(out), _stream(stream)))
+
     def sample_points(self, rays_o, rays_d, t_vals: np.ndarray, near: float, far: float, z_out, points_out=None,
                       t_rand=None, stream=None) -> None:
         t = np.ascontiguousarray(t_vals, dtype=np.float32)
@@ -285,6 +309,15 @@ class Device:
         ms = (ctypes.c_float * NERF_N_STAGES)()
         _check(self.lib.nerf_ctx_stage_ms(self._ctx, ms))
         return dict(zip(STAGES, [float(v) for v in ms]))
+
+
+def positional_encoding(precision: int, x, n_freqs: int, out, stream=None) -> None:
+    """nerf_positional_encoding: x device [n, 3] -> out device [n, 3 + 6 n_freqs] (no context needed)."""
+    lib = load_library()
+    n = x.shape[0]
+    if tuple(out.shape) != (n, 3 + 6 * n_freqs) or not (x.is_contiguous() and out.is_contiguous()):
+        raise ValueError("x [n, 3] and out [n, 3 + 6*n_freqs], contiguous")
+    _check(lib.nerf_positional_encoding(precision, _ptr(x), n, n_freqs, _ptr(out), _stream(stream)))
 
 
 def exported_symbols() -> Sequence[str]:

@@ -1,8 +1,9 @@
 """Multi-rank render check, launched by tests/test_gpu_parity.py under torchrun.
 
-Every rank renders its row band (nerf_amd.distributed.band) and the bands are
-all-gathered; rank 0 compares the gathered frame with a single-call full-frame
-render (bit-identical expected: rays are independent) and prints one JSON line.
+Every rank renders its row band (nerf_amd.distributed.band); the bands are
+all-gathered, and, separately, rendered as packed tiles and gathered to rank 0.
+Rank 0 compares both frames with a single-call full-frame render (bit-identical
+expected: rays are independent) and prints one JSON line.
 Backend from NERF_DIST_BACKEND (the test uses gloo so that two ranks can share
 one device; the 8-GPU bench uses RCCL).
 """
@@ -30,15 +31,19 @@ def main():
     pose = torch.eye(4)
     pose[2, 3] = 4.0
     w, h, s = 96, 37, 32                       # 37 rows: uneven bands
-    rgb, depth = D.render_sharded(r.render_rows, pose, (w, h), s)
+    rgb, depth = D.render_sharded(r.render_rows, pose, (w, h), s)          # all-gather of the bands
+    root = D.render_frame_to_root(r, pose, (w, h), s)                    # packed tiles gathered to rank 0
     ok = None
     if rank == 0:
         ref_rgb, ref_depth = r.render_image(pose, (w, h), s)
-        ok = bool(torch.equal(rgb, ref_rgb) and torch.equal(depth, ref_depth))
+        ok = bool(torch.equal(rgb, ref_rgb) and torch.equal(depth, ref_depth)
+                  and torch.equal(root[0], ref_rgb) and torch.equal(root[1], ref_depth))
+    else:
+        ok = root is None
         print(json.dumps({"world": world, "bands": D.bands(world, h), "identical": ok}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
-    return 0 if rank != 0 or ok else 1
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

@@ -1,0 +1,285 @@
+"""GPU parity of the reduced-precision kernels against exact restatements.
+
+The bf16 MLP (the headline benchmark's kernel) and the fp8 MLP (config 5) are
+build-defined: the reference has no such networks.  Each is pinned here against
+a float64 restatement of what it computes (``oracle.bf16_mlp_restated``,
+``oracle.fp8_mlp_restated``): the same roundings at the MFMA inputs, fed the
+kernel's own encodings (``nerf_positional_encoding`` runs the kernels' device
+code), so that the only difference left is the order of the fp32 sums inside
+the MFMAs.  The encodings themselves are pinned separately against
+``oracle.positional_encoding_fast`` and the reference's accurate sin/cos.
+
+Tolerances (written per test; measured values in DESIGN.md §4):
+  * encodings: the fp32 path within 2 ulp of torch's sin/cos; the fast path
+    within 2e-5 of its restatement and of the accurate values;
+  * bf16: the restatement adds each group of 8 products to the fp32 accumulator
+    with one rounding, as the MFMA does (tools/probes), so most samples agree bit
+    for bit; on the conditioned (chaotic, gain ~2 per layer) checkpoint a sample
+    whose fp32 sum lands within an ulp of a bf16 rounding boundary of one
+    activation can still differ, and that difference grows through the layers,
+    so the tail is bounded separately;
+  * fp8: the fp8 MFMA truncates products about 13 bits below the largest of
+    each group of 8 (tools/probes/fp8_window_probe.py), which no fp32
+    restatement reproduces; with e4m3 steps of 6 % on a crossed rounding
+    boundary the conditioned network's samples agree at the median and are
+    bounded in the tail, and a low-gain network (the nn.Linear init, where a
+    perturbation shrinks through the layers) pins the kernel's structure
+    (layouts, scales, bias tiles, k-steps) sample by sample.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from nerf_amd import runtime as rt
+from nerf_amd import weights as W
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def ckpt(tmp_path_factory):
+    p = tmp_path_factory.mktemp("ckpt_r") / "synthetic.pth"
+    return W.write_synthetic_checkpoint(str(p), seed=0)
+
+
+def _renderer(ckpt, precision):
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    r = MI355XRenderer(precision)
+    r.setup(ckpt)
+    return r
+
+
+@pytest.fixture(scope="module")
+def r16(ckpt):
+    return _renderer(ckpt, "bf16")
+
+
+@pytest.fixture(scope="module")
+def r8(ckpt):
+    return _renderer(ckpt, "fp8")
+
+
+def gpu_encoding(precision, x, n_freqs):
+    xd = torch.as_tensor(np.ascontiguousarray(x, np.float32)).cuda()
+    out = torch.empty(xd.shape[0], 3 + 6 * n_freqs, dtype=torch.float32, device="cuda")
+    rt.positional_encoding(rt.PRECISIONS[precision], xd, n_freqs, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def encodings(precision, pos, dirs):
+    """Feature-major float64 encodings as the kernel of `precision` computes them."""
+    return (gpu_encoding(precision, pos, 10).T.astype(np.float64),
+            gpu_encoding(precision, dirs, 4).T.astype(np.float64))
+
+
+def sample_errors(s_gpu, c_gpu, s_ref, c_ref):
+    """Per-sample error: max over sigma (relative to 1 + sigma) and the 3 colours."""
+    es = np.abs(s_gpu - s_ref) / (1.0 + np.abs(s_ref))
+    ec = np.abs(c_gpu - c_ref).max(axis=1)
+    return es, ec
+
+
+def report(tag, es, ec):
+    q = lambda a, p: float(np.percentile(a, p))  # noqa: E731
+    print(f"{tag}: n={es.size} sigma rel median {np.median(es):.2e} p99.9 {q(es, 99.9):.2e} max {es.max():.2e}; "
+          f"rgb median {np.median(ec):.2e} p99.9 {q(ec, 99.9):.2e} max {ec.max():.2e}")
+
+
+# ------------------------------------------------------------ encodings (a3) --
+def _points(n=20000, seed=0):
+    rng = np.random.default_rng(seed)
+    pos = rng.uniform(-10.0, 10.0, (n, 3)).astype(np.float32)      # up to the 2^9*pi*10 argument of view 1
+    dirs = rng.uniform(-1.5, 1.5, (n, 3)).astype(np.float32)
+    return pos, dirs
+
+
+def test_encoding_fp32_matches_reference_sincos(golden):
+    from oracle import nerf_oracle as O
+
+    pos, dirs = _points()
+    for x, nf in ((pos, 10), (dirs, 4), (golden("mlp")["pos"], 10)):
+        got = gpu_encoding("fp32", x, nf)
+        ref = O.positional_encoding(torch.from_numpy(np.ascontiguousarray(x)), nf).numpy()
+        ulp = np.spacing(np.maximum(np.abs(ref), np.float32(2.0 ** -126)).astype(np.float32))
+        err_ulp = np.abs(got - ref) / ulp
+        print(f"fp32 encoding L={nf}: max {np.abs(got - ref).max():.2e} ({err_ulp.max():.1f} ulp), "
+              f"bit-exact {np.mean(got == ref):.4f}")
+        assert np.array_equal(got[:, :3], ref[:, :3])
+        assert err_ulp.max() <= 2.0
+
+
+def test_encoding_fast_matches_restatement():
+    from oracle import nerf_oracle as O
+
+    pos, dirs = _points()
+    for x, nf in ((pos, 10), (dirs, 4)):
+        ref_acc = O.positional_encoding(torch.from_numpy(x), nf).numpy()
+        restated = O.positional_encoding_fast(x, nf)
+        for precision in ("bf16", "fp8"):
+            got = gpu_encoding(precision, x, nf)
+            er, ea = np.abs(got - restated), np.abs(got - ref_acc)
+            print(f"{precision} encoding L={nf}: vs restatement max {er.max():.2e} (bit-exact {np.mean(er == 0):.4f}), "
+                  f"vs accurate max {ea.max():.2e} mean {ea.mean():.2e}")
+            # v_sin/v_cos are not correctly rounded; angle doubling grows their
+            # error 2x per step, so the restatement is a bound, not bit-exact
+            assert er.max() < 2e-5 and np.median(er) < 1e-6
+            assert ea.max() < 2e-5
+
+
+# ----------------------------------------------------------------- bf16 MLP --
+def test_bf16_query_matches_restatement(r16, golden):
+    from oracle import nerf_oracle as O
+
+    g = golden("mlp")
+    pos, dirs = g["pos"], g["dirs"]
+    pe, dpe = encodings("bf16", pos, dirs)
+    c, f = W.synthetic_models(0)
+    for use_fine, sd, tag in ((True, f, "fine"), (False, c, "coarse")):
+        s_ref, rgb_ref = O.bf16_mlp_restated(sd, pe, dpe)
+        s, col = r16.query_nerf_networks(torch.from_numpy(pos), torch.from_numpy(dirs), use_fine=use_fine)
+        s = s.cpu().numpy()[:, 0]
+        es, ec = sample_errors(s, col.cpu().numpy(), s_ref, rgb_ref.T)
+        report(f"bf16 query {tag} vs restatement", es, ec)
+        print(f"  sigma bit-exact {np.mean(s == s_ref.astype(np.float32)):.4f}, samples <= 1e-5: "
+              f"{np.mean(np.maximum(es, ec) <= 1e-5):.4f}")
+        assert np.mean(s == s_ref.astype(np.float32)) >= 0.97
+        assert np.mean(np.maximum(es, ec) <= 1e-5) >= 0.995
+        assert es.max() < 2e-2 and ec.max() < 2e-3
+
+
+def _band_samples(r, row, spp=128):
+    """Rays of row `row` of the 800x600 headline frame (view 0) and their sample points."""
+    from oracle import nerf_oracle as O
+
+    g = np.load(os.path.join(GOLDEN, "render_800x600_s128_band.npz"))
+    pose = torch.from_numpy(g["poses"][0])
+    o, d = O.generate_rays(pose, 800, 600)
+    o, d = o[row].reshape(-1, 3).contiguous(), d[row].reshape(-1, 3).contiguous()
+    z = O.uniform_z(spp)
+    pts = O.sample_points(o, d, z.expand(o.shape[0], spp))
+    return pose, o, d, z, pts
+
+
+def _mlp_forward(r, precision, o, d, z, spp):
+    """nerf_mlp_forward (the render pass's MLP, unfused): (sigma, rgb) per sample."""
+    n = o.shape[0]
+    out = torch.empty(n * spp, 4, dtype=torch.float32, device="cuda")
+    r.hip.mlp_forward(rt.NERF_NET_FINE, rt.PRECISIONS[precision], o.cuda(), d.cuda(), z.cuda(), 0, n, spp, out)
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    return out[:, 0], out[:, 1:]
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_headline_band_samples_match_restatement(request, precision):
+    """Every sample of one row of the 800x600x128 headline frame (102,400 samples,
+    the benchmark's own kernel launch shape) against the restatement, and the
+    row's composited image against the restated samples composited by the oracle."""
+    from oracle import nerf_oracle as O
+
+    r = request.getfixturevalue("r16" if precision == "bf16" else "r8")
+    row, spp = 300, 128
+    pose, o, d, z, pts = _band_samples(r, row, spp)
+    pe, dpe = encodings(precision, pts.reshape(-1, 3).numpy(),
+                        d[:, None, :].expand(-1, spp, -1).reshape(-1, 3).contiguous().numpy())
+    _, f = W.synthetic_models(0)
+    restate = O.bf16_mlp_restated if precision == "bf16" else O.fp8_mlp_restated
+    s_ref, rgb_ref = restate(f, pe, dpe)
+    s_gpu, c_gpu = _mlp_forward(r, precision, o, d, z, spp)
+    es, ec = sample_errors(s_gpu, c_gpu, s_ref, rgb_ref.T)
+    report(f"{precision} headline row {row} samples vs restatement", es, ec)
+    # the composited row: oracle compositing of the restated samples vs the GPU's
+    # fused render of the same row
+    rgb_ref_img, dep_ref_img = O.composite(torch.from_numpy(s_ref.astype(np.float32)).reshape(800, spp, 1),
+                                           torch.from_numpy(rgb_ref.T.astype(np.float32)).reshape(800, spp, 3),
+                                           z.expand(800, spp), d)
+    rgb_img, dep_img = r.render_rows(pose, (800, 600), spp, row, row + 1)
+    er = float(np.abs(rgb_img.cpu().numpy().reshape(-1, 3) - rgb_ref_img.numpy()).max())
+    ed = float(np.abs(dep_img.cpu().numpy().reshape(-1) - dep_ref_img.numpy()).max())
+    print(f"{precision} headline row {row} image vs restated samples: rgb max {er:.2e} depth max {ed:.2e}")
+    exact = np.mean(s_gpu == s_ref.astype(np.float32))
+    close = np.mean(np.maximum(es, ec) <= 1e-5)
+    print(f"  sigma bit-exact {exact:.4f}, samples <= 1e-5: {close:.4f}, <= 1e-4: {np.mean(np.maximum(es, ec) <= 1e-4):.4f}")
+    if precision == "bf16":
+        assert exact >= 0.97 and close >= 0.995
+        assert es.max() < 2e-2 and ec.max() < 2e-3
+        assert er < 5e-4 and ed < 5e-3
+    else:
+        assert np.median(es) < 1e-5 and np.median(ec) < 1e-6
+        assert np.mean(np.maximum(es, ec) <= 1e-3) >= 0.8
+        assert es.max() < 1.0 and ec.max() < 5e-2
+        assert er < 1e-2 and ed < 5e-2
+
+
+# ------------------------------------------------------------------ fp8 MLP --
+def test_fp8_query_matches_restatement_tight(r8, golden):
+    """fp8 kernel vs oracle.fp8_mlp_restated on the kernel's own encodings: the
+    remaining difference is fp32 summation order, which moves a value across an
+    e4m3 rounding boundary (one 6 % step of that activation) only rarely."""
+    from oracle import nerf_oracle as O
+
+    g = golden("mlp")
+    pos, dirs = g["pos"], g["dirs"]
+    pe, dpe = encodings("fp8", pos, dirs)
+    c, f = W.synthetic_models(0)
+    for use_fine, sd, tag in ((True, f, "fine"), (False, c, "coarse")):
+        s_ref, rgb_ref = O.fp8_mlp_restated(sd, pe, dpe)
+        s, col = r8.query_nerf_networks(torch.from_numpy(pos), torch.from_numpy(dirs), use_fine=use_fine)
+        es, ec = sample_errors(s.cpu().numpy()[:, 0], col.cpu().numpy(), s_ref, rgb_ref.T)
+        report(f"fp8 query {tag} vs restatement", es, ec)
+        print(f"  samples <= 1e-4: {np.mean(np.maximum(es, ec) <= 1e-4):.4f}, <= 1e-3: "
+              f"{np.mean(np.maximum(es, ec) <= 1e-3):.4f}")
+        assert np.median(es) < 1e-5 and np.median(ec) < 1e-6
+        assert np.mean(np.maximum(es, ec) <= 1e-3) >= 0.8
+        assert es.max() < 1.0 and ec.max() < 5e-2
+
+
+# ------------------------------------------------ low-gain network (structure) --
+@pytest.fixture(scope="module")
+def tame(tmp_path_factory):
+    """nn.Linear's init without the conditioning's trunk gain: a
+    perturbation shrinks from layer to layer, so rounding-boundary crossings stay
+    local and every sample pins the kernels' structure.  Heads scaled so that sigma
+    and colour are not all saturated or zero."""
+    c = W.synthetic_state_dict(10, conditioned=False)
+    f = W.synthetic_state_dict(11, conditioned=False)
+    for sd in (c, f):
+        sd["density_head.weight"] = sd["density_head.weight"] * np.float32(30.0)
+        sd["color_layers.1.weight"] = sd["color_layers.1.weight"] * np.float32(8.0)
+    p = tmp_path_factory.mktemp("tame") / "tame.pth"
+    W.save_checkpoint(str(p), c, f)
+    return str(p), c, f
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_low_gain_network_matches_restatement(tame, golden, precision):
+    from oracle import nerf_oracle as O
+
+    path, c, f = tame
+    r = _renderer(path, precision)
+    g = golden("mlp")
+    rng = np.random.default_rng(5)
+    pos = np.concatenate([g["pos"], rng.uniform(-6, 6, (4096, 3)).astype(np.float32)])
+    dirs = np.concatenate([g["dirs"], rng.uniform(-1.2, 1.2, (4096, 3)).astype(np.float32)])
+    pe, dpe = encodings(precision, pos, dirs)
+    restate = O.bf16_mlp_restated if precision == "bf16" else O.fp8_mlp_restated
+    for use_fine, sd, tag in ((True, f, "fine"), (False, c, "coarse")):
+        s_ref, rgb_ref = restate(sd, pe, dpe)
+        s, col = r.query_nerf_networks(torch.from_numpy(pos), torch.from_numpy(dirs), use_fine=use_fine)
+        es, ec = sample_errors(s.cpu().numpy()[:, 0], col.cpu().numpy(), s_ref, rgb_ref.T)
+        report(f"{precision} low-gain net {tag} vs restatement", es, ec)
+        e = np.maximum(es, ec)
+        print(f"  samples <= 1e-6: {np.mean(e <= 1e-6):.4f}, <= 1e-5: {np.mean(e <= 1e-5):.4f}, "
+              f"<= 1e-4: {np.mean(e <= 1e-4):.4f}")
+        if precision == "bf16":
+            # one bf16 step of one colour-head input moves rgb by ~1e-4 (measured max 1.4e-4)
+            assert np.mean(e <= 1e-6) >= 0.999 and e.max() < 1e-3
+        else:
+            # the fp8 MFMA's ~2^-13 cut per group of 8 (measured: 90 % <= 1e-4)
+            assert np.median(e) <= 1e-6 and np.mean(e <= 1e-4) >= 0.85 and e.max() < 0.1

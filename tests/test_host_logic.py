@@ -129,7 +129,20 @@ def _gather_worker(rank, world, port, width, height, q):
         return rgb, rows + 0.5
 
     rgb, depth = D.render_sharded(render_rows, None, (width, height), 4)
-    q.put((rank, rgb.numpy(), depth.numpy()))
+
+    class Tiler:                  # the renderer surface render_frame_to_root uses
+        def torch_device(self):
+            return torch.device("cpu")
+
+        def render_band(self, pose, res, spp, r0, r1, out):
+            c, d = render_rows(pose, res, spp, r0, r1)
+            out[: r1 - r0, :, :3] = c
+            out[: r1 - r0, :, 3] = d
+            return out
+
+    root = D.render_frame_to_root(Tiler(), None, (width, height), 4)
+    root = None if root is None else (root[0].contiguous().numpy(), root[1].contiguous().numpy())
+    q.put((rank, rgb.numpy(), depth.numpy(), root))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -155,6 +168,11 @@ def test_band_gather_gloo_world2(height):
         assert p.exitcode == 0
     rows = np.arange(height, dtype=np.float32)[:, None].repeat(width, 1)
     cols = np.arange(width, dtype=np.float32)[None, :].repeat(height, 0)
-    for _, rgb, depth in outs:
+    for rank, rgb, depth, root in outs:
         assert np.array_equal(rgb, np.stack([rows, cols, rows * 1000 + cols], -1))
         assert np.array_equal(depth, rows + 0.5)
+        # gather of the packed band tiles to rank 0 only
+        if rank == 0:
+            assert np.array_equal(root[0], rgb) and np.array_equal(root[1], depth)
+        else:
+            assert root is None

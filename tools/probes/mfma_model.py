@@ -1,0 +1,199 @@
+"""Fit the accumulation arithmetic of the gfx950 MFMAs on the host, from the
+dataset tools/probes/mfma_dataset.py collects on the GPU box
+(gpurun_out/mfma_dataset.npz).  A model: the k products are split into groups;
+in each group every product is cut to a multiple of 2^(M - w), M the largest
+product exponent of the group (mode: toward zero, floor, or nearest), the
+group sums and the accumulator C are added exactly and rounded once to fp32."""
+import itertools
+import json
+import sys
+
+import numpy as np
+import torch
+
+
+def acc_row(i, h):
+    return (i & 3) + 8 * (i >> 2) + 4 * h
+
+
+def unpack_d(D):
+    T = D.shape[0]
+    out = np.zeros((T, 32, 32), np.float64)
+    for l in range(64):
+        for i in range(16):
+            out[:, acc_row(i, l >> 5), l & 31] = D[:, l, i]
+    return out
+
+
+def products_f8(A, B, sa, sb):
+    dec = lambda c: torch.from_numpy(np.ascontiguousarray(c)).view(torch.float8_e4m3fn).double().numpy()  # noqa: E731
+    Av, Bv = dec(A), dec(B)                                   # [T, 64 lanes, 32]
+    T = A.shape[0]
+    Am = np.zeros((T, 32, 64))
+    Bm = np.zeros((T, 64, 32))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        Am[:, r, 32 * h: 32 * h + 32] = Av[:, l]
+        Bm[:, 32 * h: 32 * h + 32, r] = Bv[:, l]
+    scale = np.exp2(sa[:, :32, None] - 127.0) * np.exp2(sb[:, None, :32] - 127.0)        # [T, 32, 32]
+    return Am[:, :, None, :] * np.swapaxes(Bm, 1, 2)[:, None, :, :] * scale[..., None]  # [T, r, c, k]
+
+
+def products_b16(A, B):
+    dec = lambda c: torch.from_numpy(np.ascontiguousarray(c)).view(torch.bfloat16).double().numpy()  # noqa: E731
+    Av, Bv = dec(A), dec(B)                                   # [T, 64, 8]
+    T = A.shape[0]
+    Am = np.zeros((T, 32, 16))
+    Bm = np.zeros((T, 16, 32))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        Am[:, r, 8 * h: 8 * h + 8] = Av[:, l]
+        Bm[:, 8 * h: 8 * h + 8, r] = Bv[:, l]
+    return Am[:, :, None, :] * np.swapaxes(Bm, 1, 2)[:, None, :, :]
+
+
+def cut(p, M, w, mode):
+    q = np.ldexp(1.0, (M - w).astype(int))
+    x = p / q
+    if mode == "zero":
+        x = np.trunc(x)
+    elif mode == "floor":
+        x = np.floor(x)
+    else:
+        x = np.rint(x)
+    return x * q
+
+
+def expo(x):
+    mag = np.abs(x)
+    return np.where(mag > 0, np.floor(np.log2(np.where(mag > 0, mag, 1.0))), -10000)
+
+
+def model(P, C, groups, w, mode, w2=None, mexp=None):
+    """P [..., K] products, C [...]; groups: list of index lists.  Group stage: each
+    product cut to 2^(M - w) (M: largest product exponent of the group, or with mexp
+    [..., K] given, the largest of those per-product exponents); final stage: the
+    group sums and C, each cut to 2^(M2 - w2) (M2 their largest exponent; w2 None:
+    exact), summed, rounded to fp32 (nearest even)."""
+    import math
+    terms = []
+    for g in groups:
+        pg = P[..., g]
+        e = expo(pg) if mexp is None else np.where(pg != 0, mexp[..., g], -10000)
+        M = e.max(-1)
+        terms.append(cut(pg, M[..., None], w, mode).sum(-1))
+    terms.append(C)
+    T = np.stack(terms, -1)
+    if w2 is not None:
+        M2 = expo(T).max(-1)
+        T = cut(T, M2[..., None], w2, "zero")
+    flat = T.reshape(-1, T.shape[-1])
+    s = np.array([math.fsum(row) for row in flat]).reshape(T.shape[:-1])
+    return s.astype(np.float32).astype(np.float64)
+
+
+def partitions(K):
+    """Candidate groupings of k (k = 32h + j for fp8, 8h + j for bf16)."""
+    half = K // 2
+    out = {}
+    for g in (1, 2, 4, 8, 16, 32, 64):
+        if g <= K:
+            out[f"contig{g}"] = [list(range(i, i + g)) for i in range(0, K, g)]
+    for g in (2, 4, 8, 16):
+        if g <= half:
+            # interleave lane halves: group i holds j-block i of both halves
+            out[f"pairhalves{g}"] = [list(range(i, i + g)) + list(range(half + i, half + i + g)) for i in range(0, half, g)]
+    return out
+
+
+def main(path="gpurun_out/mfma_dataset.npz", which=("f8", "b16")):
+    d = np.load(path)
+    tags = sorted({k.rsplit("_", 1)[0] for k in d.files})
+    res = {}
+    for tag in tags:
+        kind = tag.split("_")[0]
+        if kind not in which:
+            continue
+        n = 8                                                  # trials used for fitting (speed)
+        if kind == "f8":
+            P = products_f8(d[f"{tag}_A"][:n], d[f"{tag}_B"][:n], d[f"{tag}_sa"][:n], d[f"{tag}_sb"][:n])
+            K, ws = 64, [11, 12, 13, 14, 15]
+        else:
+            P = products_b16(d[f"{tag}_A"][:n], d[f"{tag}_B"][:n])
+            K, ws = 16, [22, 23, 24, 25, 26]
+        C = unpack_d(d[f"{tag}_C"][:n])
+        D = unpack_d(d[f"{tag}_D"][:n])
+        best = []
+        parts = {k: v for k, v in partitions(K).items() if k in ("contig8", "contig4", "contig16")}
+        w2s = [None, 22, 23, 24, 25, 26, 27, 28]
+        for (pname, groups), w, w2 in itertools.product(parts.items(), ws, w2s):
+            m = model(P, C, groups, w, "zero", w2)
+            best.append((float(np.mean(m == D)), pname, w, -1 if w2 is None else w2))
+        best.sort(reverse=True)
+        res[tag] = best[:4]
+        print(json.dumps({tag: best[:4]}), flush=True)
+    return res
+
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:2] or []))
+
+
+def cutfloat(x, b, mode):
+    """x to a float with a b-bit significand (mode: zero = truncate, near = RNE)."""
+    mag = np.abs(x)
+    e = np.floor(np.log2(np.where(mag > 0, mag, 1.0)))
+    q = np.exp2(e - b + 1)
+    y = x / q
+    y = np.trunc(y) if mode == "zero" else np.rint(y)
+    return np.where(mag > 0, y * q, 0.0)
+
+
+def model_running(P, C, g, b, mode, order="seq", final="exact"):
+    """Within each group of g consecutive k: a running sum kept as a b-bit float
+    (sequential in k, or a pairwise tree); then group sums + C exactly (final
+    'exact') or sequentially in fp32 ('seq32'), rounded to fp32."""
+    import math
+    K = P.shape[-1]
+    sums = []
+    for g0 in range(0, K, g):
+        pg = [P[..., k] for k in range(g0, g0 + g)]
+        if order == "seq":
+            s = np.zeros(P.shape[:-1])
+            for p in pg:
+                s = cutfloat(s + p, b, mode)
+        else:
+            while len(pg) > 1:
+                pg = [cutfloat(pg[i] + pg[i + 1], b, mode) for i in range(0, len(pg), 2)]
+            s = pg[0]
+        sums.append(s)
+    if final == "exact":
+        T = np.stack(sums + [C], -1)
+        flat = T.reshape(-1, T.shape[-1])
+        return np.array([math.fsum(r) for r in flat]).reshape(T.shape[:-1]).astype(np.float32).astype(np.float64)
+    acc = C.astype(np.float32)
+    for s in sums:
+        acc = (acc.astype(np.float64) + s).astype(np.float32)
+    return acc.astype(np.float64)
+
+
+def main_running(path="gpurun_out/mfma_dataset.npz"):
+    d = np.load(path)
+    tags = sorted({k.rsplit("_", 1)[0] for k in d.files})
+    for tag in tags:
+        kind = tag.split("_")[0]
+        n = 8
+        if kind == "f8":
+            P = products_f8(d[f"{tag}_A"][:n], d[f"{tag}_B"][:n], d[f"{tag}_sa"][:n], d[f"{tag}_sb"][:n])
+            gs, bs = (4, 8, 16, 64), (13, 14, 15, 16)
+        else:
+            P = products_b16(d[f"{tag}_A"][:n], d[f"{tag}_B"][:n])
+            gs, bs = (4, 8, 16), (24, 25, 26, 27)
+        C = unpack_d(d[f"{tag}_C"][:n])
+        D = unpack_d(d[f"{tag}_D"][:n])
+        best = []
+        for g, b, mode, order, final in itertools.product(gs, bs, ("zero", "near"), ("seq", "tree"), ("exact", "seq32")):
+            m = model_running(P, C, g, b, mode, order, final)
+            best.append((float(np.mean(m == D)), g, b, mode, order, final))
+        best.sort(reverse=True)
+        print(json.dumps({tag: best[:3]}), flush=True)
