@@ -15,7 +15,8 @@
 // VGPRs): activations never leave registers (nerf_layout.h).  The position and
 // direction encodings wait in LDS for the layers that take them.  (-D
 // NERF_BF16_WAVES=4 builds the one-wave-per-SIMD variant: two column tiles per
-// wave, accumulators in AGPRs.)
+// wave; it spills)  Timing ablations and the other lab variants
+// of round 1 are not part of this source.
 //
 // Quarter schedule.  Each layer is issued in quarters of two output tiles.
 // A layer's output tiles are converted to the next layer's bf16 fragments
@@ -67,21 +68,6 @@ constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;    // 256
 #ifndef NERF_BF16_PF
 #define NERF_BF16_PF 2               // fragment prefetch distance (units)
 #endif
-// Wave lag (-DNERF_BF16_LAG=1, lab): waves 4-7 run one chunk behind waves 0-3
-// (the fp8 kernel's scheme, mlp_fp8.hip); needs a ring of >= 4 slots.
-#ifndef NERF_BF16_LAG
-#define NERF_BF16_LAG 0
-#endif
-constexpr int kLagOn = NERF_BF16_LAG;
-// Deferred compositing (-DNERF_BF16_DEFER_COMP=1 or 2, lab): a tile's segment
-// composite (seg_composite) runs at the top of the next tile, after its seam,
-// (1) or beside the first MFMAs of its L0 (2), instead of in the epilogue
-// before the next tile's encodings.
-#ifndef NERF_BF16_DEFER_COMP
-#define NERF_BF16_DEFER_COMP 0
-#endif
-constexpr int kDeferComp = NERF_BF16_DEFER_COMP;   // 1: after the seam; 2: beside L0's first MFMAs
-static_assert(kCols + 1 < 4, "the deferred composite fits L0's first quarter");
 constexpr int kUnits = kHeadUnitBase + kHeadUnits;                   // 516 layer units + 12 head units
 constexpr int kChunkUnits = NERF_BF16_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitBytes;
@@ -91,23 +77,13 @@ constexpr int kPf = NERF_BF16_PF;
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // LDS-DMA pieces per wave per chunk
 constexpr int kLdsParamOff = kSlots * kChunkB;
-static_assert(kSlots >= 3 + kLagOn && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
+static_assert(kSlots >= 3 && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
 static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile: chunk g of every tile uses slot g % kSlots");
 static_assert(kTotalChunks * kChunkB <= kBf16BlobBytes, "device blob is padded for every chunk geometry");
 constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kCols * 4 * 1024;
 constexpr int kLdsSegOff = kLdsDeOff + kWaves * kCols * 2 * 1024;       // fused compositing: (dist, z) per sample
-constexpr int kLdsStampOff = kLdsSegOff + kWaves * kCols * kSamplesPerWave * 8;
-#ifdef NERF_ABLATE_DMASINK   // timing experiment: restaging lands in a chunk nobody reads
-constexpr int kLdsSinkOff = kLdsStampOff;
-#endif
-#ifdef NERF_STAMPS
-constexpr int kLdsBytes = kLdsStampOff + kWaves * (2 + 3 * kTotalChunks + 1) * 8;
-#elif defined(NERF_ABLATE_DMASINK)
-constexpr int kLdsBytes = kLdsStampOff + kChunkB;
-#else
-constexpr int kLdsBytes = kLdsStampOff;
-#endif
+constexpr int kLdsBytes = kLdsSegOff + kWaves * kCols * kSamplesPerWave * 8;
 static_assert(kLdsParamOff % 16 == 0 && kLdsPeOff % 16 == 0, "LDS carve must stay 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kGldsPerStage * kThreads * 16 == kChunkB, "stage geometry");
@@ -134,36 +110,14 @@ NL_HD int unit_extra(int n) {   // 0: B from hidden fragments (or head units); e
 
 // Chunk g -> ring slot g % kSlots.  Each wave moves its share as lane-linear
 // 1 KiB LDS-DMA pieces (destination = wave-uniform base + lane*16).
-__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane,
-                                            int lag = 0) {
-  // lag (wave-uniform 0/1): chunk g + lag of the cyclic stream, in its slot
-  const int gl = g + lag == kTotalChunks ? 0 : g + lag;
-  const int slot = g % kSlots + lag == kSlots ? 0 : g % kSlots + lag;
-#ifdef NERF_ABLATE_HOTCHUNK   // timing experiment: every chunk re-reads chunk 0 (L2-hot, wrong results)
-  const char* src = blob + wave_u * 1024 + lane * 16;
-#else
-  const char* src = blob + size_t(g) * kChunkB + wave_u * 1024 + lane * 16;
-#endif
-  char* dst = lds + slot * kChunkB + wave_u * 1024;
-#ifdef NERF_ABLATE_DMASINK
-  if (g >= kSlots) dst = lds + kLdsSinkOff + wave_u * 1024;   // the ring keeps its first fill
-#endif
+__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
+  char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i) {
-#ifdef NERF_BF16_BUILTIN_GLDS
-    __builtin_amdgcn_global_load_lds((const void*)(src + i * kThreads * 16), (lds_void*)(dst + i * kThreads * 16),
-                                     16, 0, 0);
-#else
     // issued from inline asm (nerf_asm.h): the builtin makes hipcc emit lgkmcnt(0)
     // before every fragment use; completion is tracked by counted vmcnt + barrier
-#ifdef NERF_BF16_VADDR_GLDS
-    lds_dma_16(src + i * kThreads * 16, lds_addr(dst + i * kThreads * 16));
-#else
-    (void)src;
-    lds_dma_16_s(blob + size_t(gl) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
+    lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
                  lds_addr(dst + i * kThreads * 16));
-#endif
-#endif
   }
 }
 
@@ -184,40 +138,6 @@ __device__ __forceinline__ unsigned cvt_relu_pair(float lo, float hi) {
   return __builtin_bit_cast(unsigned, m);
 }
 
-__device__ __forceinline__ bf16x8 pack8_relu(const f32x16& a, int base) {
-#if defined(NERF_ABLATE_EPILOGUE) || defined(NERF_ABLATE_LOOPONLY)
-  // timing experiment: raw bits of 4 accumulator registers (every tile stays
-  // live, so no MFMA is dead-code eliminated), no conversion, no ReLU
-  return __builtin_bit_cast(bf16x8, f32x4{a[base], a[base + 1], a[base + 2], a[base + 3]});
-#else
-  const u32x4 w{cvt_relu_pair(a[base], a[base + 1]), cvt_relu_pair(a[base + 2], a[base + 3]),
-                cvt_relu_pair(a[base + 4], a[base + 5]), cvt_relu_pair(a[base + 6], a[base + 7])};
-  return __builtin_bit_cast(bf16x8, w);
-#endif
-}
-
-// ---- diagnostic build only (-DNERF_STAMPS): s_memtime at the prologue end and
-// on both sides of every chunk barrier, per wave, for the first 256 blocks.
-// Never compiled into the shipped library; its times are not quoted, its
-// shares are (cdna_hip_programming.md §7, In-kernel stamps).
-[[maybe_unused]] constexpr int kStampSlots = 2 + 3 * kTotalChunks + 1;
-#ifdef NERF_STAMPS
-constexpr int kStampBlocks = 256;
-constexpr long kStampFirst = 8192;       // tiles; steady state: well past the cold-L2 first round
-__device__ unsigned long long g_nerf_stamps[kStampBlocks][kWaves][kStampSlots];
-// shader clock vs the 100 MHz constant clock over each wave's life (clock = dt/drt * 100 MHz)
-__device__ unsigned long long g_nerf_clock[kStampBlocks][kWaves][4];
-#define NERF_STAMP(cx, i)                                                                             \
-  do {                                                                                                \
-    __builtin_amdgcn_sched_barrier(0);                                                                \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                       \
-    if ((cx).lane == 0)                                                                               \
-      ((unsigned long long*)((cx).lds + kLdsStampOff))[(cx).wave_u * kStampSlots + (i)] = t_;         \
-    __builtin_amdgcn_sched_barrier(0);                                                                \
-  } while (0)
-#else
-#define NERF_STAMP(cx, i) do {} while (0)
-#endif
 
 struct Ctx {
   const char* blob;
@@ -227,10 +147,8 @@ struct Ctx {
   // direction encodings, and of this lane half's bias rows (asm reads add an
   // immediate offset)
   unsigned ring_addr, pe_addr, de_addr, bias_addr;
-  int lag;   // NERF_BF16_LAG: 1 for waves 4-7
 };
 
-#ifndef NERF_BF16_CC_LDS
 // ---- LDS fragment reads from inline asm with counted waits.  Left to itself
 // hipcc puts an s_waitcnt in front of almost every MFMA (one per fragment);
 // here each unit waits once, for exactly the reads it consumes: everything the
@@ -257,12 +175,10 @@ NL_HD int lgkm_for_unit(int n) {
   for (int m = n - kPf + 1; m <= n; ++m) c += bias_reads(m);
   return c;
 }
-#endif
 
 // Reads of unit n into ring entry n % kRing: two A fragments (output tiles of
 // the unit's quarter) and, for encoding inputs, the two columns' B fragments.
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols]) {
-#ifndef NERF_BF16_CC_LDS
   static_assert(kSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
   const int slot_off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes;
   ra[n % kRing][0] = ds_read_b128<bf16x8>(cx.ring_addr, slot_off);
@@ -275,21 +191,6 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
       rb[n % kRing][c] = ex == kPos ? ds_read_b128<bf16x8>(cx.pe_addr, (4 * c + u) * 1024)
                                     : ds_read_b128<bf16x8>(cx.de_addr, (2 * c + u) * 1024);
   }
-#else
-  const char* slot = cx.lds + ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitBytes + cx.lane * 16;
-  ra[n % kRing][0] = *(const bf16x8*)(slot);
-  ra[n % kRing][1] = *(const bf16x8*)(slot + 1024);
-  const int ex = unit_extra(n);
-  if (ex != 0) {
-    const int u = unit_kstep(n) - layer_shape(unit_layer(n)).hidden / 16;
-#pragma unroll
-    for (int c = 0; c < kCols; ++c) {
-      const int off = ex == kPos ? kLdsPeOff + ((cx.wave_u * kCols + c) * 4 + u) * 1024
-                                 : kLdsDeOff + ((cx.wave_u * kCols + c) * 2 + u) * 1024;
-      rb[n % kRing][c] = *(const bf16x8*)(cx.lds + off + cx.lane * 16);
-    }
-  }
-#endif
 }
 
 // Seam E_g, at the top of unit n when its prefetch (unit n+kPf) is the first
@@ -301,23 +202,16 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
 //   (3) stage chunk g+kSlots-1 into chunk g-1's slot -- past the end of the
 //       tile, the next tile's chunk of the same slot.
 // The top of a tile is seam E_-1 (tile_top).
-constexpr int kDmaOutstandingAtSeam = kSlots - 3 - kLagOn;
-constexpr int kStageAhead = kSlots - 1 - kLagOn;   // seam g stages chunk g + kStageAhead (+ the wave's lag)
+constexpr int kDmaOutstandingAtSeam = kSlots - 3;
+constexpr int kStageAhead = kSlots - 1;   // seam g stages chunk g + kStageAhead
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
   const int g = (n + kPf) / kChunkUnits - 1;
-  NERF_STAMP(cx, 2 + 3 * g);
   wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
-  NERF_STAMP(cx, 3 + 3 * g);
-#if !defined(NERF_ABLATE_BARRIER) && !defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no chunk barrier
   __builtin_amdgcn_s_barrier();
-#endif
   compiler_fence();
-  NERF_STAMP(cx, 4 + 3 * g);
-#ifndef NERF_ABLATE_NODMA   // timing experiment: the ring keeps its first chunks (real weights), wrong results
-  stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane, cx.lag);
-#endif
+  stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
 }
 // Conversion schedule (default): layer L's output tiles 2q-2, 2q-1 become final
 // at the end of its quarter q-1 and are converted to the next layer's B
@@ -338,7 +232,6 @@ __device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4&
   frag[pr & 3] = cvt_relu_pair(tile[2 * pr], tile[2 * pr + 1]);
 }
 
-#ifndef NERF_BF16_CC_LDS
 // Bias pre-load of quarter q of layer l (tiles 2q, 2q+1), straight into the
 // accumulators (param blob [layer][tile][half][16]); l, q constant after unrolling.
 __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (&acc)[kCols][8]) {
@@ -353,60 +246,31 @@ __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (
                                   b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
     }
 }
-#endif
 
-struct NoHook {
-  __device__ __forceinline__ void operator()(int, int) const {}
-};
-
-// hook(q, u): extra VALU work issued after unit (q, u)'s MFMAs (NERF_BF16_DEFER_COMP=2)
-template <int L, class Hook = NoHook>
+template <int L>
 __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[kCols][16], u32x4 (&bout)[kCols][16],
-                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], const Ctx& cx,
-                                           const Hook& hook = Hook{}) {
+                                           bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], const Ctx& cx) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
   constexpr int KU = ksteps_bf16(L);
   constexpr int NQ = out_tiles(L) / 2;
   constexpr int N0 = bf16_unit_base(L);
   constexpr bool kConvert = L != L0;          // B fragments come from the previous layer
-  [[maybe_unused]] const float* prm = (const float*)(cx.lds + kLdsParamOff);
   // outputs feed another MFMA layer: the next layer, or (C0) the heads' tile;
   // C0 has two quarters, so its tiles 2, 3 are converted in the head loop
   constexpr bool kConvertOut = true;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-#ifdef NERF_BF16_CC_LDS
-    // bias pre-load of this quarter's two output tiles (both columns)
-#pragma unroll
-    for (int o2 = 0; o2 < 2; ++o2) {
-      const f32x4* b4 = (const f32x4*)(prm + kBiasOff + 256 * L + ((2 * q + o2) * 2 + cx.h) * 16);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 b = b4[i];
-#pragma unroll
-        for (int c = 0; c < kCols; ++c)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[c][2 * q + o2][4 * i + e] = b[e];
-      }
-    }
-#endif
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int n = N0 + q * KU + u;
       seam_before(cx, n);
-#ifndef NERF_BF16_CC_LDS
       if (u == 0) issue_bias(cx, L, q, acc);   // this quarter's bias (waited with its first unit)
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
       wait_lgkm(lgkm_for_unit(n));
-#else
-      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
-#endif
-#ifndef NERF_BF16_NO_SCHED_PIN
       // keep the prefetch reads here: left alone, the scheduler sinks them next
       // to their MFMAs and every unit then waits out the LDS latency
       __builtin_amdgcn_sched_barrier(0);
-#endif
       bf16x8 b[kCols];
 #pragma unroll
       for (int c = 0; c < kCols; ++c)
@@ -417,7 +281,6 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
         for (int c = 0; c < kCols; ++c)
           acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[n % kRing][o2], b[c], acc[c][2 * q + o2],
                                                                       0, 0, 0);
-      hook(q, u);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
@@ -466,33 +329,22 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16,
                lds_base + kLdsPeOff + wave_u * kCols * 4096 + lane * 16,
                lds_base + kLdsDeOff + wave_u * kCols * 2048 + lane * 16,
-               lds_base + kLdsParamOff + h * 64, kLagOn && wave_u >= kWaves / 2 ? 1 : 0};
+               lds_base + kLdsParamOff + h * 64};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
   // Start the weight stream (chunks 0 .. kSlots-3; each tile's top stages one
   // more) and copy the parameters, once per workgroup.
 #pragma unroll
-#if defined(NERF_ABLATE_NODMA) || defined(NERF_ABLATE_DMASINK)
-  for (int g = 0; g < kSlots; ++g) stage_chunk(blob, g, lds, wave_u, lane);   // every slot real weights
-#else
-  for (int g = 0; g < kSlots - 2 - kLagOn; ++g) stage_chunk(blob, g, lds, wave_u, lane);
-#endif
+  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   const float* prm = (const float*)(lds + kLdsParamOff);
-  if (kLagOn && cx0.lag) {
-    // the lagging half's extra seam (the leading half's first tile top): chunk 0 landed, publish, stage
-    wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
-    __syncthreads();
-    stage_chunk(blob, kStageAhead - 1, lds, wave_u, lane);
-  }
 
   // A tile's results are stored at the top of the next tile, after its seam:
   // vmcnt counts stores with the LDS-DMA in issue order, so a store issued last
   // would make the next tile's first wait also wait out the store.
   f32x4 res[kCols];
   float wl[kCols];
-  f32x2_t segin[kCols];   // kDeferComp: the pending tile's (dist, z) per column
   long res_p0 = -1;
 
 #pragma unroll 1
@@ -503,10 +355,6 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     // SGPRs (spilling); recomputing each is one scalar add pair at its stage
     Ctx cx = cx0;
     asm volatile("" : "+s"(cx.blob));
-#ifdef NERF_STAMPS
-    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    NERF_STAMP(cx, 0);
     // This tile's encodings, into this wave's own LDS slots (its reads of the
     // previous tile's were waited for before their MFMAs).
 #pragma unroll 1
@@ -516,15 +364,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       float dist = 0.0f, zz = 0.0f;
       if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
       else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, seg != nullptr, x, d, dist, zz);
-#if defined(NERF_ABLATE_ENCODING) || defined(NERF_ABLATE_LOOPONLY)   // timing experiment: no sin/cos
-#pragma unroll
-      for (int q = 0; q < 32; ++q) pef[q] = x[q % 3] * float(q);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) def[q] = d[q % 3] * float(q);
-#else
       pos_encode<true>(x[0], x[1], x[2], h, pef);
       dir_encode<true>(d[0], d[1], d[2], h, def);
-#endif
       char* pe_dst = lds + kLdsPeOff + (wave_u * kCols + c) * 4096 + lane * 16;
       char* de_dst = lds + kLdsDeOff + (wave_u * kCols + c) * 2048 + lane * 16;
 #pragma unroll
@@ -541,12 +382,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     // previous chunk every wave finished with the last tile.
     wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
-    stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane, cx.lag);
-    NERF_STAMP(cx, 1);
-    if (kDeferComp == 1 && !kExplicit && seg != nullptr && res_p0 >= 0)
-#pragma unroll
-      for (int c = 0; c < kCols; ++c) res[c] = seg_composite(res[c], segin[c][0], segin[c][1], lane, wl[c]);
-    if (kDeferComp != 2 || kExplicit || seg == nullptr) store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
+    stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
+    store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
     f32x16 acc[kCols][8];
 #pragma unroll
@@ -554,19 +391,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
 
     // two B-fragment sets: layer l reads one while it fills the other for l+1
     u32x4 bA[kCols][16], bB[kCols][16];
-    if constexpr (kDeferComp == 2 && !kExplicit) {
-      // the previous tile's composite, one column per unit beside L0 quarter 0's
-      // MFMAs (L0 converts nothing there), then its stores
-      const bool pend = seg != nullptr && res_p0 >= 0;
-      auto hook = [&](int q, int u) {
-        if (q == 0 && u >= 1 && u <= kCols && pend)
-          res[u - 1] = seg_composite(res[u - 1], segin[u - 1][0], segin[u - 1][1], lane, wl[u - 1]);
-        if (q == 0 && u == kCols + 1 && seg != nullptr) store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
-      };
-      layer_bf16<L0>(acc, bB, bA, ra, rb, cx, hook);
-    } else {
-      layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
-    }
+    layer_bf16<L0>(acc, bB, bA, ra, rb, cx);
     layer_bf16<L1>(acc, bA, bB, ra, rb, cx);
     layer_bf16<L2>(acc, bB, bA, ra, rb, cx);
     layer_bf16<L3>(acc, bA, bB, ra, rb, cx);
@@ -594,14 +419,10 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     for (int i = 0; i < kHeadUnits; ++i) {
       const int n = kHeadUnitBase + i;
       seam_before(cx, n);
-#ifndef NERF_BF16_CC_LDS
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
       // head units read two fragments each and no bias: the younger reads are
       // those of the next min(kPf, units left) units (spelled out so it folds)
       wait_lgkm(2 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
-#else
-      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
-#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -624,29 +445,11 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       res[c] = f32x4{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
       if (!kExplicit && seg != nullptr) {
         const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + ((wave_u * kCols + c) * kSamplesPerWave + (lane & 31)) * 8);
-        if (kDeferComp != 0) segin[c] = in;
-        else res[c] = seg_composite(res[c], in[0], in[1], lane, wl[c]);
+        res[c] = seg_composite(res[c], in[0], in[1], lane, wl[c]);
       }
     }
     res_p0 = p0;
-#ifdef NERF_STAMPS
-    NERF_STAMP(cx, kStampSlots - 1);
-    if (tile - kStampFirst < kStampBlocks && lane == 0) {
-      unsigned long long* c = g_nerf_clock[tile - kStampFirst][wave_u];
-      c[0] = clk_t0;
-      c[1] = clk_r0;
-      c[2] = __builtin_amdgcn_s_memtime();
-      c[3] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (tile - kStampFirst < kStampBlocks && lane == 0)
-      for (int i = 0; i < kStampSlots; ++i)
-        g_nerf_stamps[tile - kStampFirst][wave_u][i] = ((unsigned long long*)(lds + kLdsStampOff))[wave_u * kStampSlots + i];
-#endif
   }
-  if (kLagOn && !cx0.lag) __builtin_amdgcn_s_barrier();   // the lagging half's last seam
-  if (kDeferComp != 0 && !kExplicit && seg != nullptr && res_p0 >= 0)
-#pragma unroll
-    for (int c = 0; c < kCols; ++c) res[c] = seg_composite(res[c], segin[c][0], segin[c][1], lane, wl[c]);
   store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
   // the stream ran kSlots-2 chunks into a tile that does not exist: let them
   // land before the workgroup's LDS is released
@@ -659,11 +462,7 @@ hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSr
                            bool explicit_points, hipStream_t stream, float* seg, float* wloc) {
   if (n_points <= 0) return hipSuccess;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
-#ifdef NERF_BF16_ONE_TILE
-  const long blocks = tiles;                        // lab: one tile per workgroup
-#else
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
-#endif
   if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)
@@ -676,19 +475,3 @@ hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSr
 }
 
 }  // namespace nerf
-
-#ifdef NERF_STAMPS
-// diagnostic build only: copy the stamps out ([256 blocks][waves][slots] u64)
-extern "C" int nerf_debug_stamps(void* host, size_t bytes, int* waves, int* slots) {
-  *waves = nerf::kWaves;
-  *slots = nerf::kStampSlots;
-  const size_t need = sizeof(nerf::g_nerf_stamps);
-  if (bytes < need) return -1;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nerf::g_nerf_stamps), need) == hipSuccess ? 0 : -2;
-}
-extern "C" int nerf_debug_clock(void* host, size_t bytes) {
-  const size_t need = sizeof(nerf::g_nerf_clock);
-  if (bytes < need) return -1;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nerf::g_nerf_clock), need) == hipSuccess ? 0 : -2;
-}
-#endif

@@ -58,22 +58,17 @@ constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
 #define NERF_FP8_SLOTS 4
 #endif
 constexpr int kSlots = NERF_FP8_SLOTS;
-// Wave lag (default; -DNERF_FP8_LAG=0 for lockstep): waves 4-7 run one chunk
-// behind waves 0-3, so the two waves of a SIMD reach their layer boundaries
-// (scale reduction and conversion, nothing for the MFMA pipe) at different
-// times.  The ring then holds one chunk more for the lagging half: every wave
-// stages one chunk less far ahead, and the lagging half's seam g is barrier
-// instance g + 1 (one extra barrier at its start, one at the leading half's
-// end).  Measured -1.6 % kernel time, bit-identical output; a 5-slot ring
-// (restoring the staging distance) was slower (-1.1 %).
-#ifndef NERF_FP8_BLOCK_SCALES
-#define NERF_FP8_BLOCK_SCALES 1     // per-sample scale per 64-row activation block (layer_fp8b); 0: one per sample
-#endif
-#ifndef NERF_FP8_LAG
-#define NERF_FP8_LAG 1
-#endif
-constexpr int kLagOn = NERF_FP8_LAG;
-static_assert(kLagOn == 0 || kSlots >= 4, "a lagged ring needs 4 slots");
+// Wave lag: waves 4-7 run one chunk behind waves 0-3, so the two waves of a
+// SIMD reach their layer boundaries (scale reduction and conversion, nothing
+// for the MFMA pipe) at different times.  The ring then holds one chunk more
+// for the lagging half: every wave stages one chunk less far ahead, and the
+// lagging half's seam g is barrier instance g + 1 (one extra barrier at its
+// start, one at the leading half's end).  Measured -1.6 % kernel time,
+// bit-identical output; a 5-slot ring (restoring the staging distance) was
+// slower (-1.1 %).  Timing ablations and other lab variants of round 1
+//  are not part of this source.
+constexpr int kLagOn = 1;
+static_assert(kSlots >= 4, "a lagged ring needs 4 slots");
 #ifndef NERF_FP8_PF
 #define NERF_FP8_PF 1   // 1: 224 VGPRs, -1.0 % against 2 (256 VGPRs); 3 spills
 #endif
@@ -166,13 +161,11 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   compiler_fence();
   __builtin_amdgcn_s_barrier();
   compiler_fence();
-#ifndef NERF_FP8_ABLATE_NODMA   // timing experiment: the ring keeps its first fill (wrong results)
   if (kLagOn) {
     if (g + cx.lag + kSlots - 2 < kTotalChunks) stage_chunk(cx, g + kSlots - 2, cx.lag);
   } else if (g + kSlots - 1 < kTotalChunks) {
     stage_chunk(cx, g + kSlots - 1);
   }
-#endif
 }
 
 __device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
@@ -204,14 +197,10 @@ __device__ __forceinline__ float i2f(int x) { return __builtin_bit_cast(float, x
 
 // Four e4m3 bytes from four fp32 values x / s (RNE), low byte first.
 __device__ __forceinline__ int cvt4_scaled(float a, float b, float c, float d, float s) {
-#ifdef NERF_FP8_ZERO_SEED
-  i16x2 w = {0, 0};
-#else
   // the low-word convert preserves the high word, which the second convert
   // overwrites: seed it with the bits of b (dying here) so the tied destination
   // takes b's register instead of a copy of a zero
   i16x2 w = __builtin_bit_cast(i16x2, b);
-#endif
   w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, a, b, s, false);
   w = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w, c, d, s, true);
   return __builtin_bit_cast(int, w);
@@ -230,38 +219,6 @@ __device__ __forceinline__ int cvt4(float a, float b, float c, float d) {
 __device__ __forceinline__ int relu_e4m3x4(int w) {
   const unsigned mask = __builtin_amdgcn_perm(unsigned(w) << 8, unsigned(w), 0x090B080Au);
   return int(~mask & unsigned(w));
-}
-
-// Tiles 2u, 2u+1 of the previous layer -> B fragment of hidden k-step u
-// (byte j: register j&15 of tile 2u + (j>>4)), divided by the sample's
-// activation scale s, converted, then ReLU'd on the bytes.
-__device__ __forceinline__ void convert_pair(const f32x16& t0, const f32x16& t1, i32x8& b, float s) {
-#if defined(NERF_FP8_ABLATE_CONVERT)   // timing experiment: raw accumulator bits, no VALU (wrong results)
-  (void)s;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    b[d] = f2i(t0[4 * d]);
-    b[4 + d] = f2i(t1[4 * d]);
-  }
-  return;
-#endif
-#ifdef NERF_FP8_RELU_F32
-  // previous form: ReLU on the fp32 bit patterns, one v_max_i32 per value
-  float v[32];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    v[i] = i2f(__builtin_elementwise_max(f2i(t0[i]), 0));
-    v[16 + i] = i2f(__builtin_elementwise_max(f2i(t1[i]), 0));
-  }
-#pragma unroll
-  for (int d = 0; d < 8; ++d) b[d] = cvt4_scaled(v[4 * d], v[4 * d + 1], v[4 * d + 2], v[4 * d + 3], s);
-#else
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    b[d] = relu_e4m3x4(cvt4_scaled(t0[4 * d], t0[4 * d + 1], t0[4 * d + 2], t0[4 * d + 3], s));
-    b[4 + d] = relu_e4m3x4(cvt4_scaled(t1[4 * d], t1[4 * d + 1], t1[4 * d + 2], t1[4 * d + 3], s));
-  }
-#endif
 }
 
 // C0's output -> bf16 B fragments of the colour k-steps (hid_bf16_feature
@@ -283,9 +240,6 @@ __device__ __forceinline__ void colour_dword(const f32x16 (&acc)[8], int t, int 
 // negative int32 and non-negative floats order like their bits, so a signed
 // integer max started at 0 is max(relu(x)) -- v_max3_i32, no NaN canonicalising.
 __device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t1) {
-#ifdef NERF_FP8_ABLATE_MAX   // timing experiment: no running maximum (wrong scales)
-  return m ^ f2i(t0[0]) ^ f2i(t1[15]);
-#endif
   // chained as max(max(m, a), b) so each pair folds into one v_max3_i32
 #pragma unroll
   for (int i = 0; i < 16; i += 2)
@@ -296,18 +250,12 @@ __device__ __forceinline__ int max_pair(int m, const f32x16& t0, const f32x16& t
   return m;
 }
 
-#if NERF_FP8_BLOCK_SCALES
 // Block scales: one activation scale per sample per 64-row block, i.e. per k-step
 // of the next layer (tiles 2v, 2v+1 -> k-step v).  Block v's scale is known as
 // soon as its two tiles are final, so a layer converts its own output one block
 // per quarter (quarters 1-3: blocks 0-2, the next layer's quarter 0: block 3)
 // into the other fragment set, and no layer waits for its whole predecessor.
 __device__ __forceinline__ int block_scale(const f32x16& t0, const f32x16& t1, float& s) {
-#ifdef NERF_FP8_ABLATE_STATIC   // timing experiment: a fixed scale (1.0), no maximum (static-scale contract)
-  (void)t0; (void)t1;
-  s = 1.0f;
-  return 127;
-#endif
   int mb = max_pair(0, t0, t1);
   const auto sw = __builtin_amdgcn_permlane32_swap(mb, mb, false, false);
   mb = __builtin_elementwise_max(int(sw[0]), int(sw[1]));
@@ -316,14 +264,6 @@ __device__ __forceinline__ int block_scale(const f32x16& t0, const f32x16& t1, f
   return 127 + e;
 }
 __device__ __forceinline__ void convert_tile(const f32x16& t, i32x8& b, int off, float s) {
-#ifdef NERF_FP8_ABLATE_STATIC   // ReLU and saturation as one v_med3_f32 per value, then the plain convert
-  const float hi = kFp8Max * s;
-#pragma unroll
-  for (int d = 0; d < 4; ++d)
-    b[off + d] = cvt4_scaled(__builtin_amdgcn_fmed3f(t[4 * d], 0.0f, hi), __builtin_amdgcn_fmed3f(t[4 * d + 1], 0.0f, hi),
-                             __builtin_amdgcn_fmed3f(t[4 * d + 2], 0.0f, hi), __builtin_amdgcn_fmed3f(t[4 * d + 3], 0.0f, hi), s);
-  return;
-#endif
 #pragma unroll
   for (int d = 0; d < 4; ++d) b[off + d] = relu_e4m3x4(cvt4_scaled(t[4 * d], t[4 * d + 1], t[4 * d + 2], t[4 * d + 3], s));
 }
@@ -392,82 +332,6 @@ __device__ __forceinline__ void layer_fp8b(f32x16 (&acc)[8], i32x8 (&bin)[4], i3
     }
   }
 }
-#endif
-
-// (C0 also leaves its activation scale in sb_out for the density k-steps and
-// converts its tiles 0, 1 to the colour fragments hb[0..3] during quarter 1.)
-template <int L>
-__device__ __forceinline__ void layer_fp8(f32x16 (&acc)[8], i32x8 (&bh)[4], i32x8 (&ra)[kRing][2],
-                                          i32x8 (&rb)[kRing], int& amax, int& sb_out, u32x4 (&hb)[8],
-                                          const Ctx& cx) {
-  constexpr LayerShape sh = layer_shape(L);
-  constexpr int KH = sh.hidden / 64;
-  constexpr int KU = ksteps_fp8(L);
-  constexpr int NQ = out_tiles(L) / 2;
-  constexpr int N0 = fp8_unit_base(L);
-  constexpr bool kConvert = L != L0;
-  constexpr bool kNextConverts = L != C0;        // the following layer reads these accumulators
-  float s = 1.0f;
-  int sb = 127;                                  // E8M0 of the activation scale (1.0 for encodings)
-  if (kConvert) {
-    // per-sample scale: the largest ReLU output of the previous layer -> [128, 256)
-    int mb = max_pair(amax, acc[6], acc[7]);
-    // the other lane half's maximum: v_permlane32_swap (VALU), not __shfl_xor,
-    // whose ds_bpermute made hipcc drain every in-flight fragment read with
-    // lgkmcnt(0) at each layer start.  Swapping mb with itself leaves, in either
-    // result, each lane's own value in one and its partner's in the other.
-    const auto sw = __builtin_amdgcn_permlane32_swap(mb, mb, false, false);
-    mb = __builtin_elementwise_max(int(sw[0]), int(sw[1]));
-    const int e = __builtin_amdgcn_frexp_expf(i2f(mb)) - 8;   // max = f * 2^(e+8), f in [0.5, 1)
-    s = __builtin_ldexpf(1.0f, e);
-    sb = 127 + e;
-    convert_pair(acc[0], acc[1], bh[0], s);
-  }
-  sb_out = sb;
-  amax = 0;
-  int sa0 = 127, sa1 = 127;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const int n = N0 + q * KU + u;
-      seam_before(cx, n);
-      if (u == 0) {
-        // bias pre-load of the quarter's two tiles (straight into the accumulators)
-        // and the E8M0 weight scales of their rows
-#pragma unroll
-        for (int o2 = 0; o2 < 2; ++o2) {
-          const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
-          const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
-          const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
-          acc[2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                                   b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
-        }
-        const u32x2 sc = ds_read_b64(cx.scale_addr, (L * 4 + q) * 512);
-        sa0 = int(sc[0]);
-        sa1 = int(sc[1]);
-      }
-      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
-      wait_lgkm(lgkm_for_unit(n));
-      const bool hidden = u < KH;
-      const i32x8 b = hidden ? bh[hidden ? u : 0] : rb[n % kRing];
-      const int sbu = hidden ? sb : 127;
-      acc[2 * q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][0], b, acc[2 * q], 0, 0, 0, sa0, 0,
-                                                                  sbu);
-      acc[2 * q + 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][1], b, acc[2 * q + 1], 0, 0, 0,
-                                                                      sa1, 0, sbu);
-      // conversion slices: tiles (2u+2, 2u+3) -> k-step u+1, before quarter 0 reads it
-      if (kConvert && q == 0 && u < 3) convert_pair(acc[2 * u + 2], acc[2 * u + 3], bh[u + 1], s);
-      if (L == C0 && q == 1) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if ((m * KU) / 16 == u) colour_dword(acc, 0, m, hb);
-      }
-      // running maximum for the next layer's scale: the previous quarter's tiles are final
-      if (kNextConverts && q >= 1 && u == (KU > 1 ? 1 : 0)) amax = max_pair(amax, acc[2 * q - 2], acc[2 * q - 1]);
-    }
-  }
-}
 
 template <bool kExplicit>
 __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __restrict__ blob,
@@ -489,11 +353,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   const long p = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
 
 #pragma unroll
-#ifdef NERF_FP8_ABLATE_NODMA
-  for (int g = 0; g < kSlots; ++g) stage_chunk(cx, g);   // every slot real weights
-#else
   for (int g = 0; g < kSlots - 1 - kLagOn; ++g) stage_chunk(cx, g);
-#endif
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   for (int i = threadIdx.x; i < kFp8ScaleBytes / 16; i += kThreads)
@@ -535,20 +395,14 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     compiler_fence();
     __builtin_amdgcn_s_barrier();
     compiler_fence();
-#ifndef NERF_FP8_ABLATE_NODMA
     stage_chunk(cx, kSlots - 2);
-#endif
   }
-#if defined(NERF_FP8_PRIO)   // lab: static priority 1 for waves 4-7 (1) or 0-3 (2)
-  if ((NERF_FP8_PRIO == 1) == (wave_u >= kWaves / 2)) __builtin_amdgcn_s_setprio(1);
-#endif
   i32x8 ra[kRing][2], rb[kRing];
 #pragma unroll
   for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
 
   f32x16 acc[8];
   u32x4 hb[8];
-#if NERF_FP8_BLOCK_SCALES
   // two fragment sets: layer l reads one while it fills the other for l+1
   i32x8 bA[4], bB[4];
   int sA[4] = {127, 127, 127, 127}, sB[4] = {127, 127, 127, 127};
@@ -562,19 +416,6 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   layer_fp8b<L7>(acc, bA, bB, sA, sB, ra, rb, hb, cx);
   layer_fp8b<C0>(acc, bB, bA, sB, sA, ra, rb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
   i32x8 (&bh)[4] = bB;                                   // C0's input: the density k-steps
-#else
-  i32x8 bh[4];
-  int amax = 0, sb = 127;
-  layer_fp8<L0>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L1>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L2>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L3>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L4>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L5>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L6>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<L7>(acc, bh, ra, rb, amax, sb, hb, cx);
-  layer_fp8<C0>(acc, bh, ra, rb, amax, sb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
-#endif
 
   // Heads (nerf.py:114, 123-129) as one MFMA tile: row 3 density (fp8 k-steps
   // over bh, C0's input, at C0's activation scale), rows 0-2 colour (bf16
@@ -598,13 +439,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     if (i < kFp8DensityUnits) {
 #pragma unroll
       for (int o2 = 0; o2 < 2; ++o2)
-#if NERF_FP8_BLOCK_SCALES
         hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
                                                                0, sB[2 * i + o2]);
-#else
-        hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
-                                                               0, sb);
-#endif
 #pragma unroll
       for (int m = 0; m < 16; ++m)
         if (m / 8 == i) colour_dword(acc, 2, m, hb);

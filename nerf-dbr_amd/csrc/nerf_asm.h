@@ -62,39 +62,20 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
 #undef NERF_VM
 }
 
-// One lane-linear 1 KiB LDS-DMA piece per wave: 16 B per lane from src to
-// LDS byte address lds_base + lane*16 (wave-uniform base in M0, saved and
-// restored inside the statement).  Completion is tracked with vmcnt.
-__device__ __forceinline__ void lds_dma_16(const void* src, unsigned lds_base) {
-  unsigned keep;
-  const unsigned base = __builtin_amdgcn_readfirstlane(lds_base);
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(base)
-      : "memory");
-}
-
-// The same piece in saddr form: address = SGPR base (wave-uniform 64-bit) +
-// a per-lane 32-bit VGPR offset, so advancing through a stream costs scalar
-// adds instead of a 64-bit VALU add per piece.
+// One lane-linear 1 KiB LDS-DMA piece per wave, in saddr form: 16 B per lane
+// from SGPR base (wave-uniform 64-bit) + a per-lane 32-bit VGPR offset to LDS
+// byte address lds_base + lane*16 (wave-uniform base in M0), so advancing
+// through a stream costs scalar adds instead of a 64-bit VALU add per piece.
+// Completion is tracked with vmcnt.
+// M0 is written without save/restore: hipcc treats M0 as reserved and ignores
+// the clobber (-Winline-asm), so the library build checks that nothing else in
+// the MFMA kernels reads or writes M0 (Makefile target check-m0, run by every
+// build; it fails the build otherwise).
 __device__ __forceinline__ void lds_dma_16_s(const void* sbase, unsigned voff, unsigned lds_base) {
-  unsigned keep;
   const unsigned base = __builtin_amdgcn_readfirstlane(lds_base);
   const unsigned long long sb = (unsigned long long)sbase;
   const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(sb)), hi = __builtin_amdgcn_readfirstlane(unsigned(sb >> 32));
   const unsigned long long s64 = (unsigned long long)lo | ((unsigned long long)hi << 32);
-#ifndef NERF_M0_SAVE
-  // M0 handed to the compiler as clobbered (default): no save/restore when
-  // nothing else in the kernel keeps a value there (-DNERF_M0_SAVE: the
-  // save/restore form below)
-  // hipcc treats M0 as reserved and ignores the clobber (-Winline-asm); the
-  // build checks that nothing else in the kernels touches M0 (make check-m0).
-  (void)keep;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
   asm volatile(
@@ -105,17 +86,6 @@ __device__ __forceinline__ void lds_dma_16_s(const void* sbase, unsigned voff, u
       : "v"(voff), "s"(s64), "s"(base)
       : "memory", "m0");
 #pragma clang diagnostic pop
-  return;
-#endif
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(s64), "s"(base)
-      : "memory");
 }
 
 }  // namespace nerf

@@ -117,9 +117,12 @@ class BaseUnifiedRenderer(ABC):
     def get_device_info(self) -> str:
         return f"CPU - {psutil.cpu_count()} cores"
 
-    @abstractmethod
+    # The reference gives these three a generic torch body; here the concrete
+    # renderer supplies them (this package computes nothing outside the HIP
+    # library), so the base raises.  Abstract are exactly the reference's two.
     def query_nerf_networks(self, positions, directions, use_fine: bool = True):
         """(density [N,1], rgb [N,3]) of the shared network (base_renderer.py:165-188)."""
+        raise NotImplementedError(f"{type(self).__name__} does not implement query_nerf_networks")
 
     @abstractmethod
     def execute_volume_rendering(self, densities, colors, z_vals, ray_directions):
@@ -129,10 +132,10 @@ class BaseUnifiedRenderer(ABC):
     def render_image(self, camera_pose, resolution: Tuple[int, int], samples_per_ray: int = 64):
         """(rgb [H,W,3], depth [H,W]) (base_renderer.py:207-221)."""
 
-    @abstractmethod
     def generate_rays(self, camera_pose, width: int, height: int, focal: float = 800.0):
         """(rays_o, rays_d), each [H,W,3] (base_renderer.py:223-258)."""
+        raise NotImplementedError(f"{type(self).__name__} does not implement generate_rays")
 
-    @abstractmethod
     def sample_points_on_rays(self, rays_o, rays_d, n_samples: int = 64):
         """(points [N,S,3], z [N,S]) (base_renderer.py:260-281)."""
+        raise NotImplementedError(f"{type(self).__name__} does not implement sample_points_on_rays")

@@ -643,3 +643,38 @@ def test_render_band_packed_matches_render_rows(ckpt, precision, spp, n_imp):
     torch.cuda.synchronize()
     assert torch.equal(tile[: r1 - r0, :, :3], rgb) and torch.equal(tile[: r1 - r0, :, 3], depth)
     assert bool((tile[r1 - r0:] == -7.0).all())
+
+
+def test_cli_benchmark_only_on_gpu(tmp_path):
+    """main.py --benchmark_only (the reference CLI's benchmark mode, main.py:112-262)
+    on a small grid: the CSV with the reference's columns (benchmark_suite.py:244-255),
+    sample renders per renderer and the performance plot."""
+    import subprocess
+    import sys
+
+    import pandas as pd
+
+    from nerf_amd.benchmark.benchmark_suite import CSV_COLUMNS
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "out"
+    res = subprocess.run([sys.executable, os.path.join(repo, "nerf-dbr_amd", "main.py"), "--benchmark_only",
+                          "--synthetic-checkpoint", "--checkpoint", str(tmp_path / "ckpt.pth"),
+                          "--resolutions", "64x48,100x75", "--spp", "16,32", "--views", "2",
+                          "--precisions", "fp32,bf16,fp8", "--hierarchical", "64", "--output_dir", str(out)],
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    df = pd.read_csv(out / "benchmark_results.csv")
+    assert list(df.columns) == CSV_COLUMNS
+    assert len(df) == 4 * 2 * 2                                      # 4 renderers x 2 resolutions x 2 spp
+    assert set(df["Resolution"]) == {"64x48", "100x75"} and set(df["Samples/Ray"]) == {16, 32}
+    assert (df["Rays/Second"] > 0).all()
+    for _, row in df.iterrows():
+        w, h = map(int, row["Resolution"].split("x"))
+        assert row["Rays/Second"] == pytest.approx(w * h / row["Render Time (s)"], rel=1e-6)
+        assert "gfx950" in row["Device Info"]
+    for name in df["Method"].unique():
+        d = out / "sample_renders" / name.replace(" ", "_")
+        for v in (0, 1):
+            assert (d / f"view_{v}_rgb.png").exists() and (d / f"view_{v}_depth.png").exists()
+    assert (out / "performance_comparison.png").exists()

@@ -176,3 +176,64 @@ def test_band_gather_gloo_world2(height):
             assert np.array_equal(root[0], rgb) and np.array_equal(root[1], depth)
         else:
             assert root is None
+
+
+# ---------------------------------------- plugin interface vs the reference --
+def _sig_fixture():
+    import json
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "plugin_signatures.json")) as f:
+        return json.load(f)
+
+
+def _check_conforms(cls, ref_methods, skip=()):
+    import inspect
+
+    for name, spec in ref_methods.items():
+        if name in skip:
+            continue
+        assert hasattr(cls, name), f"{cls.__name__} lacks {name}"
+        ours = list(inspect.signature(getattr(cls, name)).parameters.values())
+        ref = spec["params"]
+        # the reference's parameters, in order and with the same defaults, then
+        # only optional extras
+        assert [p.name for p in ours[: len(ref)]] == [p["name"] for p in ref], (cls.__name__, name)
+        for p, rp in zip(ours, ref):
+            if rp["default"] is not None:
+                assert p.default is not inspect.Parameter.empty and repr(p.default) == rp["default"], (name, p.name)
+        for p in ours[len(ref):]:
+            assert p.default is not inspect.Parameter.empty or p.kind == p.VAR_KEYWORD, (name, p.name)
+
+
+def test_plugin_signatures_match_reference():
+    """MI355XRenderer and the restated base class against the reference's
+    BaseUnifiedRenderer / SharedNeRFModel signatures (tests/golden/plugin_signatures.json,
+    generated from /root/reference/src/benchmark/base_renderer.py:16-281)."""
+    import inspect
+
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    fx = _sig_fixture()
+    _check_conforms(B.BaseUnifiedRenderer, fx["BaseUnifiedRenderer"])
+    _check_conforms(B.SharedNeRFModel, fx["SharedNeRFModel"])
+    # the plugin: every method (its constructor takes only optional arguments, as
+    # the reference's concrete renderers do, so the suite can build it bare)
+    _check_conforms(MI355XRenderer, fx["BaseUnifiedRenderer"], skip=("__init__",))
+    init = inspect.signature(MI355XRenderer.__init__).parameters
+    assert all(p.default is not inspect.Parameter.empty for n, p in init.items() if n != "self")
+    # the abstract methods are implemented
+    for name, spec in fx["BaseUnifiedRenderer"].items():
+        if spec["abstract"]:
+            assert not getattr(getattr(MI355XRenderer, name), "__isabstractmethod__", False), name
+
+    class Probe(B.BaseUnifiedRenderer):
+        def execute_volume_rendering(self, *a):
+            pass
+
+        def render_image(self, *a):
+            pass
+
+    probe = Probe("probe", "cpu")
+    assert set(fx["BaseUnifiedRenderer.__init__.attributes"]) <= set(vars(probe))
+    for k, v in fx["BaseUnifiedRenderer.__init__.values"].items():
+        assert repr(getattr(probe, k)) == v, k
