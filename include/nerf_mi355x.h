@@ -44,6 +44,10 @@ enum nerf_precision {
                     scales, per-sample activation scales, f32 accumulate; the
                     compressed-weights path (config 5; the reference's int8
                     CompressedNeRFRenderer, src/benchmark/compressed_renderer.py) */
+  NERF_BF16X3 = 3, /* split bf16 on the bf16 MFMA: W.X ~ Wh.Xh + Wh.Xl + Wl.Xh with
+                      v = vh + vl, vh = bf16(v), vl = bf16(v - vh); f32 accumulate,
+                      accurate encodings: the parity-grade fast path (RGB/depth
+                      within the 1e-4 gate of the reference renderer) */
 };
 
 enum nerf_net { NERF_NET_COARSE = 0, NERF_NET_FINE = 1 };
@@ -82,6 +86,11 @@ int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob,
 size_t nerf_fp8_blob_bytes(void);
 int nerf_pack_weights_fp8(const float* const* params, int n_params, uint8_t* blob);
 void nerf_f32_to_e4m3(const float* x, int n, uint8_t* out);
+
+/* Pure host helper for the split-bf16 path: W_hi / W_lo fragment units the
+ * NERF_BF16X3 kernel streams (nerf_layout.h kBf16x3BlobBytes). */
+size_t nerf_bf16x3_blob_bytes(void);
+int nerf_pack_weights_bf16x3(const float* const* params, int n_params, uint16_t* blob);
 
 /* Pure host helper: z = near*(1-t) + far*t in fp32, operation for operation
  * (src/benchmark/base_renderer.py:274-275). */
@@ -169,7 +178,7 @@ int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, 
  * encodings (n_freqs 10: positions, 4: directions): x device [n][3] -> out device
  * [n][3 + 6*n_freqs] = [x, sin(2^0 pi x), cos(2^0 pi x), sin(2^1 pi x), ...] -- the values
  * the MLP kernels of `precision` compute before rounding them to the MFMA's input type.
- * NERF_FP32: accurate sincosf of fl(2^k*pi)*x (the parity path); NERF_BF16 / NERF_FP8: one
+ * NERF_FP32 / NERF_BF16X3: accurate sincosf of fl(2^k*pi)*x; NERF_BF16 / NERF_FP8: one
  * reduced sin/cos per coordinate and lane half, then angle doubling (nerf_device.h). */
 int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream);
 

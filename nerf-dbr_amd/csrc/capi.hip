@@ -46,6 +46,7 @@ struct NetDev {
   float* f32 = nullptr;
   void* bf16 = nullptr;
   void* fp8 = nullptr;      // e4m3 fragments + E8M0 row scales (nerf_layout.h)
+  void* bf16x3 = nullptr;   // split-bf16 fragments: W_hi and W_lo units (nerf_layout.h)
   float* params = nullptr;
   bool loaded = false;
 };
@@ -108,7 +109,7 @@ int grow(T*& p, size_t& cap, size_t need, const char* what) {
 int check_net(nerf_ctx* ctx, int net, int precision) {
   if (!ctx) return set_error(NERF_E_INVALID, "null context");
   if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
-  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8)
+  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8 && precision != NERF_BF16X3)
     return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (!ctx->net[net].loaded) return set_error(NERF_E_NO_WEIGHTS, "%s network not loaded", net ? "fine" : "coarse");
   return NERF_OK;
@@ -130,6 +131,7 @@ hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, 
   const NetDev& nd = ctx->net[net];
   if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg, wloc);
+  if (precision == NERF_BF16X3) return launch_mlp_bf16x3(nd.bf16x3, nd.params, src, n, out, expl, s);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
 }
 
@@ -178,6 +180,7 @@ void nerf_ctx_destroy(nerf_ctx* ctx) {
     if (nd.f32) (void)hipFree(nd.f32);
     if (nd.bf16) (void)hipFree(nd.bf16);
     if (nd.fp8) (void)hipFree(nd.fp8);
+    if (nd.bf16x3) (void)hipFree(nd.bf16x3);
     if (nd.params) (void)hipFree(nd.params);
   }
   for (float* p : {ctx->rays, ctx->mlp_out, ctx->zbuf, ctx->wbuf})
@@ -202,13 +205,18 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
   const size_t nfp8 = nerf_fp8_blob_bytes();
   std::vector<uint8_t> f8(nfp8);
   if ((rc = nerf_pack_weights_fp8(params, n_params, f8.data())) != NERF_OK) return rc;
+  const size_t nx3 = nerf_bf16x3_blob_bytes();
+  std::vector<uint16_t> x3(nx3 / 2);
+  if ((rc = nerf_pack_weights_bf16x3(params, n_params, x3.data())) != NERF_OK) return rc;
   DeviceGuard g(ctx->device);
   NetDev& nd = ctx->net[net];
   if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
   if (!nd.bf16) HIP_TRY(hipMalloc(&nd.bf16, nbf16));
   if (!nd.params) HIP_TRY(hipMalloc((void**)&nd.params, nprm));
   if (!nd.fp8) HIP_TRY(hipMalloc(&nd.fp8, nfp8));
+  if (!nd.bf16x3) HIP_TRY(hipMalloc(&nd.bf16x3, nx3));
   HIP_TRY(hipMemcpy(nd.fp8, f8.data(), nfp8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(nd.bf16x3, x3.data(), nx3, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.f32, f32.data(), nf32, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.bf16, bf.data(), nbf16, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));
@@ -454,7 +462,8 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
     // sampler scales them by the earlier segments' transmittance; otherwise the
     // (sigma, rgb) buffer and the sequential composite kernel (the coarse image
     // itself is not an output of render_image)
-    const bool fuse_coarse = (ctx->fused_composite & 2) && precision != NERF_FP32 && n_samples % 32 == 0 &&
+    const bool fuse_coarse = (ctx->fused_composite & 2) && (precision == NERF_BF16 || precision == NERF_FP8) &&
+                             n_samples % 32 == 0 &&
                              n_importance <= 1024;
     SampleSrc src{rays_o, rays_d, z_first, z_first_stride, n_samples, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s,
@@ -480,7 +489,8 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
   // bf16 / fp8 with whole 32-sample segments per ray: compositing fused into the
   // MLP epilogue (one record per segment), then chained per ray; the fp32 parity
   // path keeps the sequential composite kernel
-  const bool fused = (ctx->fused_composite & 1) && precision != NERF_FP32 && n_fine > 1 && n_fine % 32 == 0;
+  const bool fused = (ctx->fused_composite & 1) && (precision == NERF_BF16 || precision == NERF_FP8) && n_fine > 1 &&
+                     n_fine % 32 == 0;
   {
     SampleSrc src{rays_o, rays_d, z_main, z_stride, n_fine, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s,
@@ -534,14 +544,14 @@ int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, 
 }
 
 int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream) {
-  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8)
+  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8 && precision != NERF_BF16X3)
     return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (n < 0 || (n_freqs != kPosL && n_freqs != kDirL))
     return set_error(NERF_E_INVALID, "nerf_positional_encoding: n %ld, n_freqs %d (the model's are 10 and 4)", n,
                      n_freqs);
   if (n == 0) return NERF_OK;
   if (!x || !out) return set_error(NERF_E_INVALID, "nerf_positional_encoding: null pointer");
-  HIP_TRY(launch_encode(x, n, n_freqs, precision != NERF_FP32, out, (hipStream_t)stream));
+  HIP_TRY(launch_encode(x, n, n_freqs, precision == NERF_BF16 || precision == NERF_FP8, out, (hipStream_t)stream));
   return NERF_OK;
 }
 

@@ -1,0 +1,356 @@
+// Split-bf16 ("bf16x3") NeRF MLP on gfx950: the parity-grade fast path.
+//
+// Replaces NeRFModel.forward (src/models/nerf.py:92-131) fused with
+// sample_points_on_rays (src/benchmark/base_renderer.py:260-281) and the
+// positional encoding (nerf.py:24-45), like mlp_f32.hip, but on the bf16 MFMA
+// (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate): every fp32 operand v is
+// split into v_hi = bf16(v) and v_lo = bf16(v - v_hi), and each product is
+//     W.X ~= W_hi.X_hi + W_hi.X_lo + W_lo.X_hi
+// (the dropped W_lo.X_lo is ~2^-16 relative), accumulated in fp32.  Measured
+// against the reference PyTorch-CPU renderer this stays well inside the 1e-4
+// RGB/depth gate, at three bf16 MFMAs per product.
+//
+// Structure: mlp_bf16.hip's (transposed Linear, accumulators become the next
+// layer's B fragments, quarter schedule, LDS ring filled by LDS-DMA with one
+// barrier per chunk, persistent tiles, asm fragment reads with counted waits),
+// with one wave per SIMD: a lane holds the layer's 8 accumulator tiles (128)
+// and the previous and next layers' hi and lo fragments (4 x 64), which only
+// fits in the 512-entry register file of a single wave (accumulators in AGPRs).
+//   * 4 waves x 32 samples = 128 samples per workgroup tile;
+//   * weight units of 4 KiB = the bf16 kernel's 2 KiB unit of W_hi, then W_lo
+//     (nerf_pack_weights_bf16x3), 4 units per 16 KiB chunk, 3-slot ring;
+//   * encodings are the accurate fp32 ones (the fp32 path's sincosf), split
+//     into hi and lo fragments in LDS;
+//   * the ReLU'd fp32 activations are split as they are converted:
+//     hi = bf16(relu x), lo = bf16(relu x - hi).
+// Outputs (sigma, r, g, b) per sample; the render pass composites with the
+// sequential kernel (the fp32 path's).
+#include "nerf_asm.h"
+#include "nerf_device.h"
+#include "nerf_internal.h"
+
+namespace nerf {
+namespace {
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;            // 128
+constexpr int kUnits = kHeadUnitBase + kHeadUnits;                    // 516 layer units + 12 head units
+constexpr int kUnitB = 2 * kUnitBytes;                                // 4 KiB: hi unit, lo unit
+constexpr int kChunkUnits = 4;
+constexpr int kChunkB = kChunkUnits * kUnitB;                         // 16 KiB
+constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;   // 132
+constexpr int kSlots = 3;
+constexpr int kPf = 2;                                                // fragment prefetch distance (units)
+constexpr int kRing = kPf + 1;
+constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // 4 LDS-DMA pieces per wave per chunk
+static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile: chunk g always uses slot g % kSlots");
+static_assert(kTotalChunks * kChunkB <= kBf16x3BlobBytes, "device blob is padded for the chunk geometry");
+static_assert(kGldsPerStage * kThreads * 16 == kChunkB, "stage geometry");
+constexpr int kLdsParamOff = kSlots * kChunkB;
+constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
+constexpr int kPeWaveB = 2 * 4 * 1024;                                // hi, lo x 4 k-steps x 1 KiB
+constexpr int kDeWaveB = 2 * 2 * 1024;                                // hi, lo x 2 k-steps x 1 KiB
+constexpr int kLdsDeOff = kLdsPeOff + kWaves * kPeWaveB;
+constexpr int kLdsBytes = kLdsDeOff + kWaves * kDeWaveB;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+static_assert((kSlots - 1) * kChunkB + (kChunkUnits - 1) * kUnitB + 3 * 1024 < 65536, "ds_read offsets");
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// ---- compile-time unit map, as a constexpr table (this kernel is large
+// enough that the optimiser stops folding mlp_bf16.hip's loop-based map) ----
+struct UnitInfo {
+  int layer, kstep, extra, reads, lgkm;
+  bool opens;
+};
+struct UnitTable {
+  UnitInfo u[kUnits];
+};
+constexpr UnitTable make_unit_table() {
+  UnitTable t{};
+  for (int n = 0; n < kUnits; ++n) {
+    UnitInfo& x = t.u[n];
+    if (n >= kHeadUnitBase) {
+      x = UnitInfo{-1, n - kHeadUnitBase, 0, 4, 0, false};
+      continue;
+    }
+    int l = 0;
+    while (l + 1 < kNumMfmaLayers && bf16_unit_base(l + 1) <= n) ++l;
+    const int ks = (n - bf16_unit_base(l)) % ksteps_bf16(l);
+    const int ex = ks < layer_shape(l).hidden / 16 ? 0 : layer_shape(l).extra;
+    x = UnitInfo{l, ks, ex, 4 + (ex != 0 ? 2 : 0), 0, ks == 0};
+  }
+  constexpr int kBiasReads = 8;   // 2 tiles x 4 x 16 B
+  // LDS reads younger than everything unit n consumes, at its wait: the issue
+  // order per unit body m is [bias reads if m opens a quarter], reads of unit
+  // m+kPf, wait, MFMAs (the prologue issued units 0..kPf-1)
+  for (int n = 0; n < kUnits; ++n) {
+    int c = 0;
+    if (t.u[n].opens) {
+      c = n + kPf < kUnits ? t.u[n + kPf].reads : 0;
+    } else {
+      for (int k = n + 1; k <= n + kPf; ++k) c += k < kUnits ? t.u[k].reads : 0;
+      for (int m = n - kPf + 1; m <= n; ++m) c += m >= 0 && t.u[m].opens ? kBiasReads : 0;
+    }
+    t.u[n].lgkm = c;
+  }
+  return t;
+}
+constexpr UnitTable kTab = make_unit_table();
+
+struct Ctx {
+  const char* blob;
+  char* lds;
+  int wave_u, lane, h;
+  unsigned ring_addr, pe_addr, de_addr, bias_addr;
+};
+
+__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
+  char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i)
+    lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
+                 lds_addr(dst + i * kThreads * 16));
+}
+
+// fp32 -> (hi, lo) bf16 parts of two values, packed: hi = bf16(v), lo = bf16(v - hi)
+__device__ __forceinline__ void split_pair(float a, float b, unsigned& hi, unsigned& lo) {
+  const bf16x2 p = __builtin_convertvector(f32x2{a, b}, bf16x2);                     // v_cvt_pk_bf16_f32
+  hi = __builtin_bit_cast(unsigned, p);
+  const float ha = __builtin_bit_cast(float, hi << 16), hb = __builtin_bit_cast(float, hi & 0xFFFF0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{__fsub_rn(a, ha), __fsub_rn(b, hb)}, bf16x2));
+}
+__device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    unsigned h2, l2;
+    split_pair(v[2 * d], v[2 * d + 1], h2, l2);
+    hi[d] = h2;
+    lo[d] = l2;
+  }
+}
+
+// Reads of unit n into ring entry n % kRing: A_hi and A_lo of the unit's two
+// output tiles and, for encoding inputs, the B fragment's hi and lo.
+__device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRing][4], bf16x8 (&rb)[kRing][2]) {
+  const int off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<bf16x8>(cx.ring_addr, off + f * 1024);
+  const int ex = kTab.u[n].extra;
+  if (ex != 0) {
+    const int u = kTab.u[n].kstep - layer_shape(kTab.u[n].layer).hidden / 16;
+    if (ex == kPos) {
+      rb[n % kRing][0] = ds_read_b128<bf16x8>(cx.pe_addr, u * 1024);
+      rb[n % kRing][1] = ds_read_b128<bf16x8>(cx.pe_addr, 4096 + u * 1024);
+    } else {
+      rb[n % kRing][0] = ds_read_b128<bf16x8>(cx.de_addr, u * 1024);
+      rb[n % kRing][1] = ds_read_b128<bf16x8>(cx.de_addr, 2048 + u * 1024);
+    }
+  }
+}
+
+constexpr int kDmaOutstandingAtSeam = kSlots - 3;
+constexpr int kStageAhead = kSlots - 1;
+__device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
+  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
+  const int g = (n + kPf) / kChunkUnits - 1;
+  wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
+  compiler_fence();
+  __builtin_amdgcn_s_barrier();
+  compiler_fence();
+  stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
+}
+
+// Conversion schedule of mlp_bf16.hip: one dword (two values) per unit.
+NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
+NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
+__device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4& fhi, u32x4& flo) {
+  unsigned h2, l2;
+  split_pair(relu(tile[2 * pr]), relu(tile[2 * pr + 1]), h2, l2);
+  fhi[pr & 3] = h2;
+  flo[pr & 3] = l2;
+}
+
+__device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (&acc)[8]) {
+#pragma unroll
+  for (int o2 = 0; o2 < 2; ++o2) {
+    const int off = 4 * (kBiasOff + 256 * l + (2 * q + o2) * 32);
+    const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
+    const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
+    acc[2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                             b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma3(const bf16x8& ahi, const bf16x8& alo, const bf16x8& bhi, const bf16x8& blo,
+                                        f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc, 0, 0, 0);
+}
+
+// One layer: reads the previous layer's fragments (ih/il), fills the next's (oh/ol).
+template <int L>
+__device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
+                                         u32x4 (&ol)[16], bf16x8 (&ra)[kRing][4], bf16x8 (&rb)[kRing][2],
+                                         const Ctx& cx) {
+  constexpr LayerShape sh = layer_shape(L);
+  constexpr int KH = sh.hidden / 16;
+  constexpr int KU = ksteps_bf16(L);
+  constexpr int NQ = out_tiles(L) / 2;
+  constexpr int N0 = bf16_unit_base(L);
+  constexpr bool kConvert = L != L0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int n = N0 + q * KU + u;
+      seam_before(cx, n);
+      if (u == 0) issue_bias(cx, L, q, acc);
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      wait_lgkm(kTab.u[n].lgkm);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool hid = u < KH;
+      const bf16x8 bhi = hid ? __builtin_bit_cast(bf16x8, ih[hid ? u : 0]) : rb[n % kRing][0];
+      const bf16x8 blo = hid ? __builtin_bit_cast(bf16x8, il[hid ? u : 0]) : rb[n % kRing][1];
+#pragma unroll
+      for (int o2 = 0; o2 < 2; ++o2)
+        acc[2 * q + o2] = mfma3(ra[n % kRing][o2], ra[n % kRing][2 + o2], bhi, blo, acc[2 * q + o2]);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int t = m >> 3, pr = m & 7;
+        if (kConvert && q == 0 && u == dword_unit_in(m))
+          convert_dword(acc[6 + t], pr, ih[2 * (6 + t) + (pr >> 2)], il[2 * (6 + t) + (pr >> 2)]);
+        if (q >= 1 && u == dword_unit_out(KU, m))
+          convert_dword(acc[2 * q - 2 + t], pr, oh[2 * (2 * q - 2 + t) + (pr >> 2)], ol[2 * (2 * q - 2 + t) + (pr >> 2)]);
+      }
+    }
+  }
+}
+
+template <bool kExplicit>
+__global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __restrict__ blob,
+                                                                 const float* __restrict__ prm_g, SampleSrc src,
+                                                                 long n_points, f32x4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  const int lane = threadIdx.x & 63;
+  const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  const unsigned lds_base = lds_addr(lds);
+  const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16, lds_base + kLdsPeOff + wave_u * kPeWaveB + lane * 16,
+                lds_base + kLdsDeOff + wave_u * kDeWaveB + lane * 16, lds_base + kLdsParamOff + h * 64};
+  const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+
+#pragma unroll
+  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+  for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
+    ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
+  const float* prm = (const float*)(lds + kLdsParamOff);
+
+  f32x4 res = {};
+  long res_p0 = -1;
+#pragma unroll 1
+  for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const long p0 = (tile * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
+    Ctx cx = cx0;
+    asm volatile("" : "+s"(cx.blob));   // keep the 132 chunk addresses out of SGPRs across tiles
+    {
+      float x[3], d[3], pef[32], def[16];
+      fetch_sample<kExplicit>(src, p0 < n_points ? p0 : n_points - 1, x, d);
+      pos_encode<false>(x[0], x[1], x[2], h, pef);    // accurate sincosf, as the fp32 path
+      dir_encode<false>(d[0], d[1], d[2], h, def);
+      char* pe_dst = lds + kLdsPeOff + wave_u * kPeWaveB + lane * 16;
+      char* de_dst = lds + kLdsDeOff + wave_u * kDeWaveB + lane * 16;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        u32x4 hi, lo;
+        split8(pef + 8 * u, hi, lo);
+        *(u32x4*)(pe_dst + u * 1024) = hi;
+        *(u32x4*)(pe_dst + 4096 + u * 1024) = lo;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        u32x4 hi, lo;
+        split8(def + 8 * u, hi, lo);
+        *(u32x4*)(de_dst + u * 1024) = hi;
+        *(u32x4*)(de_dst + 2048 + u * 1024) = lo;
+      }
+    }
+    wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
+    __syncthreads();
+    stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
+    if (res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
+    bf16x8 ra[kRing][4], rb[kRing][2];
+    f32x16 acc[8];
+#pragma unroll
+    for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+
+    u32x4 aH[16], aL[16], bH[16], bL[16];
+    layer_x3<L0>(acc, bH, bL, aH, aL, ra, rb, cx);
+    layer_x3<L1>(acc, aH, aL, bH, bL, ra, rb, cx);
+    layer_x3<L2>(acc, bH, bL, aH, aL, ra, rb, cx);
+    layer_x3<L3>(acc, aH, aL, bH, bL, ra, rb, cx);
+    layer_x3<L4>(acc, bH, bL, aH, aL, ra, rb, cx);   // skip: [x, pe] (nerf.py:109-110)
+    layer_x3<L5>(acc, aH, aL, bH, bL, ra, rb, cx);
+    layer_x3<L6>(acc, bH, bL, aH, aL, ra, rb, cx);
+    layer_x3<L7>(acc, aH, aL, bH, bL, ra, rb, cx);
+    layer_x3<C0>(acc, bH, bL, aH, aL, ra, rb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+
+    // Heads (nerf.py:114, 123-129): one tile, density row 3 over L7's fragments
+    // (bH/bL, C0's input, k-steps 0..15), colour rows 0-2 over C0's output
+    // (aH/aL: tiles 0, 1 converted in C0's quarter 1, tiles 2, 3 below).
+    f32x16 hacc = f32x16{};
+    if (h == 0) {
+      hacc[0] = prm[kC1B];
+      hacc[1] = prm[kC1B + 1];
+      hacc[2] = prm[kC1B + 2];
+      hacc[3] = prm[kSigB];
+    }
+#pragma unroll
+    for (int i = 0; i < kHeadUnits; ++i) {
+      const int n = kHeadUnitBase + i;
+      seam_before(cx, n);
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      wait_lgkm(4 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int k = 2 * i + s2;
+        const bf16x8 bhi = __builtin_bit_cast(bf16x8, k < 16 ? bH[k < 16 ? k : 0] : aH[k >= 16 ? k - 16 : 0]);
+        const bf16x8 blo = __builtin_bit_cast(bf16x8, k < 16 ? bL[k < 16 ? k : 0] : aL[k >= 16 ? k - 16 : 0]);
+        hacc = mfma3(ra[n % kRing][s2], ra[n % kRing][2 + s2], bhi, blo, hacc);
+      }
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (i < 8 && m / 2 == i)
+          convert_dword(acc[2 + (m >> 3)], m & 7, aH[2 * (2 + (m >> 3)) + ((m & 7) >> 2)],
+                        aL[2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
+    }
+    res = f32x4{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
+    res_p0 = p0;
+  }
+  if (res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
+  wait_vmcnt(0);   // the stream ran into a tile that does not exist: let it land
+}
+
+}  // namespace
+
+hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
+                             bool explicit_points, hipStream_t stream) {
+  if (n_points <= 0) return hipSuccess;
+  const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
+  const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
+  if (explicit_points)
+    hipLaunchKernelGGL(mlp_bf16x3_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
+                       (f32x4*)out);
+  else
+    hipLaunchKernelGGL(mlp_bf16x3_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
+                       (f32x4*)out);
+  return hipGetLastError();
+}
+
+}  // namespace nerf

@@ -35,6 +35,9 @@ hipError_t launch_mlp_bf16(const void* blob, const float* params, const SampleSr
 hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points,
                           float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr,
                           float* wloc = nullptr);
+// Split-bf16 parity-grade path (mlp_bf16x3.hip): (sigma, r, g, b) per sample.
+hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points,
+                             float* out, bool explicit_points, hipStream_t stream);
 // Chains each ray's segment records into (rgb, depth) (nerf_device.h SegRecord).
 hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
                                      hipStream_t stream, OutStrides os = {});

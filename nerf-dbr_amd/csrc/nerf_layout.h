@@ -164,6 +164,9 @@ NL_HD int head_k_row_col(int u, int row, int h, int j, int* spec_is_density) {
 // Packed bf16 blob size: units rounded up to a multiple of 32 (zero padding),
 // so any kernel chunk geometry of up to 32 units reads inside the buffer.
 constexpr int kBf16BlobBytes = ((kHeadUnitBase + kHeadUnits + 31) / 32) * 32 * kUnitBytes;
+// Split-bf16 blob (mlp_bf16x3.hip): for each bf16 unit, its W_hi = bf16(W) unit
+// then its W_lo = bf16(W - W_hi) unit (4 KiB per unit, same padding).
+constexpr int kBf16x3BlobBytes = 2 * kBf16BlobBytes;
 
 // ------------------------------------------------------------------ fp8 --
 // v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 A and B (OCP e4m3fn).  Lane half h

@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "nerf_layout.h"
 #include "nerf_mi355x.h"
@@ -59,7 +60,60 @@ int row_scale_exp(float max_abs) {
   return e < -127 ? -127 : (e > 127 ? 127 : e);
 }
 
+// The bf16 blob's values before rounding (fp32), in stream order: per layer
+// [quarter][k-step][tile-in-quarter][lane][8], then the heads' tile
+// (nerf_layout.h); padding slots are 0.
+void bf16_stream_values(const float* const* params, std::vector<float>& out) {
+  auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * kSpecIn[spec] + k]; };
+  out.clear();
+  out.reserve(size_t(kBf16BlobBytes) / 2);
+  for (int l = 0; l < kNumMfmaLayers; ++l) {
+    const int spec = kSpecOfLayer[l], nq = out_tiles(l) / 2, ku = ksteps_bf16(l);
+    for (int q = 0; q < nq; ++q)
+      for (int u = 0; u < ku; ++u)
+        for (int o2 = 0; o2 < 2; ++o2)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+              const int col = bf16_k_col(l, u, lane >> 5, j);
+              const int row = 32 * (2 * q + o2) + (lane & 31);
+              out.push_back(col < 0 ? 0.0f : W(spec, row, col));
+            }
+  }
+  for (int u = 0; u < kHeadKsteps; ++u)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int j = 0; j < 8; ++j) {
+        int dens = 0;
+        const int row = lane & 31;
+        const int f = head_k_row_col(u, row, lane >> 5, j, &dens);
+        out.push_back(f < 0 ? 0.0f : (dens ? W(kSpecDensity, 0, f) : W(kSpecColor1, row, f)));
+      }
+}
+
 }  // namespace
+
+extern "C" size_t nerf_bf16x3_blob_bytes(void) { return size_t(kBf16x3BlobBytes); }
+
+extern "C" int nerf_pack_weights_bf16x3(const float* const* params, int n_params, uint16_t* blob) {
+  if (!params || n_params != NERF_N_PARAMS || !blob)
+    return set_error(NERF_E_INVALID, "nerf_pack_weights_bf16x3: need %d tensors and a blob", NERF_N_PARAMS);
+  for (int i = 0; i < NERF_N_PARAMS; ++i)
+    if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_bf16x3: tensor %d is NULL", i);
+  std::vector<float> vals;
+  bf16_stream_values(params, vals);
+  constexpr size_t kUnit = size_t(kUnitBytes) / 2;          // bf16 elements per bf16 unit
+  std::memset(blob, 0, size_t(kBf16x3BlobBytes));
+  for (size_t i = 0; i < vals.size(); ++i) {
+    const uint16_t hi = f32_to_bf16_rne(vals[i]);
+    uint32_t hb = uint32_t(hi) << 16;
+    float hf;
+    std::memcpy(&hf, &hb, 4);
+    const uint16_t lo = f32_to_bf16_rne(vals[i] - hf);     // exact in fp32
+    const size_t unit = i / kUnit, off = i % kUnit;
+    blob[(2 * unit) * kUnit + off] = hi;
+    blob[(2 * unit + 1) * kUnit + off] = lo;
+  }
+  return NERF_OK;
+}
 
 extern "C" size_t nerf_fp8_blob_bytes(void) { return size_t(kFp8BlobBytes); }
 
@@ -158,30 +212,10 @@ extern "C" int nerf_pack_weights(const float* const* params, int n_params, float
     }
   }
   if (bf16_blob) {
-    uint16_t* dst = bf16_blob;
-    for (int l = 0; l < kNumMfmaLayers; ++l) {
-      const int spec = kSpecOfLayer[l], nq = out_tiles(l) / 2, ku = ksteps_bf16(l);
-      for (int q = 0; q < nq; ++q)
-        for (int u = 0; u < ku; ++u)
-          for (int o2 = 0; o2 < 2; ++o2)
-            for (int lane = 0; lane < 64; ++lane)
-              for (int j = 0; j < 8; ++j) {
-                const int col = bf16_k_col(l, u, lane >> 5, j);
-                const int row = 32 * (2 * q + o2) + (lane & 31);
-                *dst++ = col < 0 ? uint16_t(0) : f32_to_bf16_rne(W(spec, row, col));
-              }
-    }
-    // the heads' tile (nerf_layout.h kHeadUnits)
-    for (int u = 0; u < kHeadKsteps; ++u)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int j = 0; j < 8; ++j) {
-          int dens = 0;
-          const int row = lane & 31;
-          const int f = head_k_row_col(u, row, lane >> 5, j, &dens);
-          *dst++ = f < 0 ? uint16_t(0) : f32_to_bf16_rne(dens ? W(kSpecDensity, 0, f) : W(kSpecColor1, row, f));
-        }
-    uint16_t* end = bf16_blob + size_t(kBf16BlobBytes) / 2;
-    while (dst < end) *dst++ = 0;
+    std::vector<float> vals;
+    bf16_stream_values(params, vals);
+    for (size_t i = 0; i < vals.size(); ++i) bf16_blob[i] = f32_to_bf16_rne(vals[i]);
+    for (size_t i = vals.size(); i < size_t(kBf16BlobBytes) / 2; ++i) bf16_blob[i] = 0;
   }
   if (param_blob) {
     std::memset(param_blob, 0, sizeof(float) * kParamFloats);

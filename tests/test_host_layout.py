@@ -347,3 +347,33 @@ def test_fp8_packing_computes_the_mlp(samples):
     s_dir, rgb_dir = O.fp8_mlp_restated(sd, pe[:, :6], dpe[:, :6], chain=False)
     np.testing.assert_allclose(s_emu, s_dir, rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(rgb_emu, rgb_dir, rtol=1e-6, atol=1e-6)
+
+
+# ---------------------------------------------------------- split-bf16 path --
+def test_bf16x3_packing_splits_the_bf16_stream():
+    """nerf_pack_weights_bf16x3: unit n of the split blob is the bf16 blob's unit n
+    rounded (W_hi, bit-identical to the bf16 packing) followed by the rounded
+    remainder (W_lo = bf16(W - W_hi)); hi + lo carries W to 2^-16 relative."""
+    sd = W.synthetic_state_dict(2)
+    _, bf, _ = rt.pack_weights(sd)
+    x3 = rt.pack_weights_bf16x3(sd)
+    unit = 1024                                        # bf16 elements per 2 KiB unit
+    n_units = bf.size // unit
+    assert x3.size == 2 * bf.size
+    u3 = x3.reshape(n_units, 2, unit)
+    assert np.array_equal(u3[:, 0], bf.reshape(n_units, unit))
+    hi, lo = bf16_to_f32(u3[:, 0]), bf16_to_f32(u3[:, 1])
+    # the fp32 values of the stream, from the fp32 packing of the same weights
+    # through the hi/lo identity: |W - (hi + lo)| <= 2^-17 |W| (lo is RNE of an exact remainder)
+    w_rec = hi.astype(np.float64) + lo
+    nz = hi != 0
+    rel = np.abs(lo[nz] / hi[nz])
+    assert rel.max() <= 2.0 ** -8 + 1e-12                # a remainder is below half a bf16 ulp of hi
+    assert np.all(np.isfinite(w_rec))
+    # every non-padding weight of the network appears with its split in the blob
+    flat = np.concatenate([sd[f"layers.{i}.weight"].ravel() for i in range(8)])
+    hi_w = round_bf16(flat).astype(np.float64)
+    lo_w = round_bf16((flat.astype(np.float64) - hi_w).astype(np.float32))
+    recon = set(np.round((hi_w + lo_w) * 2 ** 30).astype(np.int64).tolist())
+    got = set(np.round(w_rec[nz] * 2 ** 30).astype(np.int64).tolist())
+    assert recon <= got | {0}
