@@ -20,9 +20,9 @@ cd /tmp
 ARGS="--precision $PREC --cpu-seconds 0 --no-error-check --no-extras"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run \
   -- python3 $ROOT/bench.py --steps 10 --warmup 3 $ARGS > "$OUT/bench_under_rocprof.json" 2> "$OUT/trace.log" || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT/pmc_fetch" -o run \
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT/pmc_fetch" -o run \
   -- python3 $ROOT/bench.py --steps 2 --warmup 1 $ARGS > "$OUT/pmc_fetch.log" 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$OUT/pmc_write" -o run \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$OUT/pmc_write" -o run \
   -- python3 $ROOT/bench.py --steps 2 --warmup 1 $ARGS > "$OUT/pmc_write.log" 2>&1 || exit $?
 echo "$ARGS" > "$OUT/command.txt"
 echo "profiles in $OUT"
