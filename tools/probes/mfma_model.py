@@ -81,6 +81,7 @@ def model(P, C, groups, w, mode, w2=None, mexp=None):
         pg = P[..., g]
         e = expo(pg) if mexp is None else np.where(pg != 0, mexp[..., g], -10000)
         M = e.max(-1)
+        M = np.where(M > -1000, M, 0)                 # an all-zero group sums to 0
         terms.append(cut(pg, M[..., None], w, mode).sum(-1))
     terms.append(C)
     T = np.stack(terms, -1)
