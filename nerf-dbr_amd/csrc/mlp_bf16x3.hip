@@ -37,11 +37,22 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;            // 128
 constexpr int kUnits = kHeadUnitBase + kHeadUnits;                    // 516 layer units + 12 head units
 constexpr int kUnitB = 2 * kUnitBytes;                                // 4 KiB: hi unit, lo unit
-constexpr int kChunkUnits = 4;
+// Ring geometry (compile-time knobs, swept with tools/kernel_lab.py; make variant)
+#ifndef NERF_X3_CHUNK_UNITS
+#define NERF_X3_CHUNK_UNITS 4
+#endif
+#ifndef NERF_X3_SLOTS
+#define NERF_X3_SLOTS 3
+#endif
+#ifndef NERF_X3_PF
+#define NERF_X3_PF 2
+#endif
+constexpr int kChunkUnits = NERF_X3_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitB;                         // 16 KiB
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;   // 132
-constexpr int kSlots = 3;
-constexpr int kPf = 2;                                                // fragment prefetch distance (units)
+constexpr int kSlots = NERF_X3_SLOTS;
+constexpr int kPf = NERF_X3_PF;                                       // fragment prefetch distance (units)
+static_assert(kSlots >= 3 && kPf <= kChunkUnits, "prefetch reaches at most one published chunk ahead");
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // 4 LDS-DMA pieces per wave per chunk
 static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile: chunk g always uses slot g % kSlots");
@@ -54,7 +65,11 @@ constexpr int kDeWaveB = 2 * 2 * 1024;                                // hi, lo 
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kPeWaveB;
 constexpr int kLdsBytes = kLdsDeOff + kWaves * kDeWaveB;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
-static_assert((kSlots - 1) * kChunkB + (kChunkUnits - 1) * kUnitB + 3 * 1024 < 65536, "ds_read offsets");
+// ds_read offsets are 16 bits: slots below kLoSlots are read at ring_addr + offset,
+// the rest at ring_hi_addr (= ring_addr + kLoSlots * kChunkB) + offset
+constexpr int kLoSlots = 65536 / kChunkB < kSlots ? 65536 / kChunkB : kSlots;
+static_assert(kChunkB <= 32768 && (kSlots - kLoSlots) * kChunkB <= 65536, "ds_read offsets");
+static_assert(kGldsPerStage >= 1, "at least one LDS-DMA piece per wave per chunk");
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -105,7 +120,7 @@ struct Ctx {
   const char* blob;
   char* lds;
   int wave_u, lane, h;
-  unsigned ring_addr, pe_addr, de_addr, bias_addr;
+  unsigned ring_addr, pe_addr, de_addr, bias_addr, ring_hi_addr;
 };
 
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
@@ -136,9 +151,11 @@ __device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
 // Reads of unit n into ring entry n % kRing: A_hi and A_lo of the unit's two
 // output tiles and, for encoding inputs, the B fragment's hi and lo.
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRing][4], bf16x8 (&rb)[kRing][2]) {
-  const int off = ((n / kChunkUnits) % kSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
+  const int slot = (n / kChunkUnits) % kSlots;
+  const unsigned base = slot < kLoSlots ? cx.ring_addr : cx.ring_hi_addr;
+  const int off = (slot < kLoSlots ? slot : slot - kLoSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
 #pragma unroll
-  for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<bf16x8>(cx.ring_addr, off + f * 1024);
+  for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<bf16x8>(base, off + f * 1024);
   const int ex = kTab.u[n].extra;
   if (ex != 0) {
     const int u = kTab.u[n].kstep - layer_shape(kTab.u[n].layer).hidden / 16;
@@ -241,7 +258,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
   const int h = lane >> 5;
   const unsigned lds_base = lds_addr(lds);
   const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16, lds_base + kLdsPeOff + wave_u * kPeWaveB + lane * 16,
-                lds_base + kLdsDeOff + wave_u * kDeWaveB + lane * 16, lds_base + kLdsParamOff + h * 64};
+                lds_base + kLdsDeOff + wave_u * kDeWaveB + lane * 16, lds_base + kLdsParamOff + h * 64,
+                lds_base + kLoSlots * kChunkB + lane * 16};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
 #pragma unroll
