@@ -1,0 +1,69 @@
+"""The training-step restatement (oracle/nerf_train_oracle.py) against the
+reference's own NeRFTrainer (tests/golden/train.npz, make_golden_train.py).
+CPU only."""
+import numpy as np
+import pytest
+
+from oracle import nerf_train_oracle as T
+from nerf_amd import weights as W
+
+
+@pytest.fixture(scope="module")
+def fx(golden):
+    return golden("train")
+
+
+@pytest.fixture(scope="module")
+def run(fx):
+    """The oracle fed the reference's recorded draws: per-step losses and lrs, the
+    clipped gradients after step 1 and the parameters after step 3."""
+    sd_c, sd_f = W.synthetic_models(0)
+    cfg = dict(T.TRAIN_CONFIG, n_rays=int(fx["n_rays"]))
+    orc = T.TrainOracle(sd_c, sd_f, cfg)
+    losses, lrs, grads = [], [], None
+    for s in range(3):
+        loss = orc.backward(fx["image"], fx["pose"], float(fx["focal"]), fx[f"step{s}_select"], fx[f"step{s}_t_rand"])[0]
+        orc.clip()
+        if s == 0:
+            grads = [orc.grads(0), orc.grads(1)]
+        orc.update()
+        losses.append(loss)
+        lrs.append(orc.lr)
+    return losses, lrs, grads, [orc.params_np(0), orc.params_np(1)]
+
+
+def test_trainer_rays_bit_exact(fx):
+    ro, rd = T.trainer_rays(fx["pose"], *fx["image"].shape[:2], float(fx["focal"]))
+    assert np.array_equal(ro.numpy(), fx["rays_o"])
+    assert np.array_equal(rd.numpy(), fx["rays_d"])
+
+
+def test_train_losses_and_lr(fx, run):
+    losses, lrs, _, _ = run
+    for s in range(3):
+        # the same torch ops in the same order on the same inputs: bit-identical
+        assert losses[s] == float(fx[f"step{s}_loss"]), s
+        assert lrs[s] == float(fx[f"step{s}_lr"])
+
+
+def test_train_clipped_grads_step1(fx, run):
+    _, _, grads, _ = run
+    for n, net in enumerate(("coarse", "fine")):
+        for k in T.PARAM_ORDER:
+            g = grads[n][k].ravel()
+            ref = fx[f"grad1_{net}_{k}"]
+            idx = np.unique(np.concatenate([np.arange(min(g.size, 256)), np.arange(0, g.size, 61)]))
+            assert np.array_equal(g[idx], ref), (net, k)
+            st = fx[f"grad1_{net}_{k}_stats"]
+            assert np.sqrt((g.astype(np.float64) ** 2).sum()) == st[2], (net, k)
+
+
+def test_train_params_after_three_steps(fx, run):
+    _, _, _, params = run
+    for n, net in enumerate(("coarse", "fine")):
+        for k in T.PARAM_ORDER:
+            v = params[n][k].ravel()
+            ref = fx[f"param3_{net}_{k}"]
+            idx = np.unique(np.concatenate([np.arange(min(v.size, 256)), np.arange(0, v.size, 61)]))
+            assert np.array_equal(v[idx], ref), (net, k)
+            assert v.astype(np.float64).sum() == fx[f"param3_{net}_{k}_stats"][0], (net, k)
