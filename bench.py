@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-error-check", action="store_true", help="skip the bf16-vs-fp32 error band")
     ap.add_argument("--no-extras", action="store_true", help="skip the other BASELINE configs and the grid")
     ap.add_argument("--no-grid", action="store_true", help="skip the README resolution x spp grid")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-step leg")
+    ap.add_argument("--train-steps", type=int, default=10)
     return ap.parse_args()
 
 
@@ -206,6 +208,87 @@ def sharded_hierarchical(ckpt, pose, local, rank, world, width, height, n_warm=2
     return {"rays_per_s": width * height / dt, "ms_per_frame": 1e3 * dt, "n_gpus": world,
             "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)",
             "parallelism": f"row-band x{world} + {dist.get_backend()} gather to rank 0"}
+
+
+# ---------------------------------------------------------------- training --
+TRAIN_RAYS = 2048            # main.py:40 (get_default_config n_rays)
+
+
+def training_leg(local, n_steps, cpu_seconds):
+    """NeRFTrainer.train_step on this GPU with main.py's configuration
+    (2048 rays, 64 stratified coarse + 128 uniform fine samples, Adam lr 3e-4, weight
+    decay 1e-6, clip 1.0): steps/s and rays/s with the step's own draws (torch.randperm,
+    torch.rand on the device) inside the timed region, the GEMMs' fp32 MFMA rate from
+    the trainer's HIP events, and the oracle's step timed on the host cores."""
+    import numpy as np
+    import torch
+
+    from nerf_amd import weights as W
+    from nerf_amd.trainer import MI355XTrainer
+    from oracle import nerf_train_oracle as T
+
+    cfg = dict(T.TRAIN_CONFIG, n_rays=TRAIN_RAYS)
+    sd_c, sd_f = W.synthetic_models(0)
+    tr = MI355XTrainer(cfg, sd_c, sd_f, device_index=local)
+    h = w = 400
+    rng = np.random.RandomState(3)
+    image = torch.from_numpy(rng.rand(h, w, 3).astype(np.float32)).cuda(local)
+    pose = torch.eye(4)
+    pose[2, 3] = 4.0
+    batch = {"image": image, "pose": pose, "focal": 0.5 * w / np.tan(0.5 * 0.6911112070083618)}
+    tr.set_profiling(True)
+    losses = [tr.train_step(batch) for _ in range(2)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stages = []
+    for _ in range(n_steps):
+        tr.train_step(batch, sync=False)
+        stages.append(tr.stage_ms())
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n_steps
+    losses.append(tr.train_step(batch))
+    st = {k: float(np.mean([s[k] for s in stages])) for k in stages[0]}
+    gemm_ms = st["forward_gemm"] + st["backward_gemm"]
+    flop = tr.gemm_flops()
+    out = {"workload": "NeRFTrainer.train_step, main.py config: 2048 rays of a 400x400 target, 64 stratified "
+                       "coarse + 128 uniform fine samples, both nets forward+backward, clip 1.0, Adam, ExponentialLR",
+           "dtype": "fp32", "steps": n_steps, "ms_per_step": 1e3 * dt, "steps_per_s": 1.0 / dt,
+           "rays_per_s": TRAIN_RAYS / dt, "stage_ms": st,
+           "gemm": {"flop_per_step": flop, "ms_per_step": gemm_ms, "achieved": flop / (gemm_ms * 1e-3) / 1e12,
+                    "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                    "frac": flop / (gemm_ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"],
+                    "note": "all forward, backward-data and weight-gradient GEMMs of both nets (unpadded "
+                            "MACs x 2) over the forward_gemm + backward_gemm stages (HIP events)"},
+           "loss_first_last": [losses[0], losses[-1]]}
+    tr.close()
+    if cpu_seconds > 0:
+        # the oracle's step (PyTorch-CPU autograd restatement of NeRFTrainer.train_step)
+        import math
+
+        info = host_cpu_info()
+        threads = info["physical_affinity"]
+        if info["cgroup_quota_cpus"]:
+            threads = max(1, min(threads, int(math.floor(info["cgroup_quota_cpus"]))))
+        prev = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        try:
+            n_cpu = 256
+            orc = T.TrainOracle(sd_c, sd_f, dict(cfg, n_rays=n_cpu))
+            img = image.cpu().numpy()
+            draws = [(rng.permutation(h * w)[:n_cpu], rng.rand(n_cpu, 64).astype(np.float32)) for _ in range(8)]
+            orc.step(img, pose.numpy(), batch["focal"], *draws[0])
+            t0 = time.perf_counter()
+            k = 0
+            while k < len(draws) - 1 and (k == 0 or time.perf_counter() - t0 < cpu_seconds):
+                orc.step(img, pose.numpy(), batch["focal"], *draws[k + 1])
+                k += 1
+            cdt = (time.perf_counter() - t0) / k
+        finally:
+            torch.set_num_threads(prev)
+        out["cpu_baseline"] = {"value": n_cpu / cdt, "unit": "rays/s", "cores": threads, "kind": "port",
+                               "sample": f"oracle TrainOracle.step, {k} steps of {n_cpu} rays (64 + 128 samples), "
+                                         f"{threads} torch threads", "ms_per_step": 1e3 * cdt}
+    return out
 
 
 # ------------------------------------------------------------- CPU baseline --
@@ -397,6 +480,9 @@ def main():
                 rs[p].setup(ckpt)
                 rs[p].hip.set_profiling(True)
         extra["readme_grid"] = readme_grid(rs, pose, rank, world)
+
+    if world == 1 and not args.no_train:
+        extra["training"] = training_leg(local, args.train_steps, min(10.0, args.cpu_seconds / 3))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

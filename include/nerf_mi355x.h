@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NERF_ABI_VERSION 1
+#define NERF_ABI_VERSION 2
 
 enum nerf_status {
   NERF_OK = 0,
@@ -95,6 +95,10 @@ int nerf_pack_weights_bf16x3(const float* const* params, int n_params, uint16_t*
 /* Pure host helper: z = near*(1-t) + far*t in fp32, operation for operation
  * (src/benchmark/base_renderer.py:274-275). */
 void nerf_uniform_z(const float* t_vals, int n, float near_, float far_, float* z_out);
+
+/* Pure host helper: torch.linspace(0, 1, n) as torch's CPU kernel computes it, bit for bit
+ * (the t table of src/utils/rendering.py:37 and base_renderer.py:274). */
+void nerf_linspace01(int n, float* out);
 
 /* Replaces: BaseUnifiedRenderer.generate_rays (src/benchmark/base_renderer.py:223-258)
  * for image rows [row0, row1).  c2w: 16 floats row-major [4][4] (host).  Outputs are
@@ -212,6 +216,72 @@ int nerf_ctx_stage_ms_history(nerf_ctx* ctx, int n, float* ms_out /* [n][NERF_N_
  *   (sigma, rgb) per sample and runs the sequential composite kernel for both. */
 #define NERF_OPT_FUSED_COMPOSITE 1
 int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value);
+
+/* ---------------------------------------------------------------------------------------
+ * Training: NeRFTrainer's step on the device, fp32 throughout
+ * (f32-in MFMA GEMMs, exact fp32 fma chains).  A trainer owns both networks' fp32
+ * parameters, their gradients, Adam's moment estimates and the lr schedule.
+ * ------------------------------------------------------------------------------------- */
+
+/* NeRFTrainer's configuration (src/training/trainer.py:25-81; main.py:25-61 defaults). */
+typedef struct nerf_train_config {
+  double lr;           /* optim.Adam lr (trainer.py:57)                                  */
+  double beta1, beta2; /* Adam betas (torch defaults 0.9, 0.999)                          */
+  double eps;          /* Adam eps (torch default 1e-8)                                   */
+  double weight_decay; /* Adam L2 weight decay added to the gradient (trainer.py:58)      */
+  double lr_gamma;     /* ExponentialLR gamma = lr_decay ** (1 / decay_steps) (:62-64)    */
+  double grad_clip;    /* clip_grad_norm_ max_norm over both nets; <= 0: no clipping (:128-133) */
+  int n_coarse;        /* stratified coarse samples per ray (:66, rendering.py:17-52)      */
+  int n_fine;          /* uniform fine samples per ray (:67, trainer.py:307-309)          */
+  float near_, far_;   /* scene bounds (:70-71)                                           */
+} nerf_train_config;
+
+typedef struct nerf_trainer nerf_trainer;
+
+/* Replaces: NeRFTrainer.__init__ (trainer.py:25-81) with the state dicts loaded: coarse and
+ * fine are the 22 host tensors of each NeRFModel in state-dict order (NERF_N_PARAMS). */
+int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* const* coarse,
+                        const float* const* fine, int n_params, nerf_trainer** out);
+void nerf_trainer_destroy(nerf_trainer* tr);
+
+/* Replaces: NeRFTrainer.train_step (trainer.py:83-138) -- _get_rays (:271-292), the ray
+ * selection (:106-114), _render_rays (:294-316: coarse samples stratified by
+ * VolumeRenderer.sample_points_on_rays(perturb=True), rendering.py:17-52; fine samples uniform),
+ * _query_network + volume_render (:318-351, rendering.py:102-143), the two MSE losses,
+ * backward, clip_grad_norm_, Adam and ExponentialLR (:121-136).  The step's draws are inputs:
+ *   image   device [height][width][3] target colours;
+ *   c2w     host 16 floats row-major [4][4]; focal as the dataset's (loader.py:36);
+ *   select  device int32 [n_rays] = torch.randperm(height*width)[:n_rays] (trainer.py:111);
+ *   t_rand  device [n_rays][n_coarse] = the coarse pass's torch.rand_like (rendering.py:47).
+ * loss_out (device [3], may be NULL): loss, coarse MSE, fine MSE.  flags: NERF_TRAIN_NO_UPDATE
+ * stops after backward (gradients unclipped, no optimizer or schedule step). */
+#define NERF_TRAIN_NO_UPDATE 1
+int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width, float focal,
+                    const float* c2w, const int32_t* select, int n_rays, const float* t_rand, int flags,
+                    float* loss_out, void* stream);
+
+/* Reads one net's state into 22 host buffers (state-dict order and shapes; synchronous):
+ * what = NERF_TR_PARAMS, NERF_TR_GRADS (the last step's gradients, clipped when that step
+ * updated), NERF_TR_EXP_AVG or NERF_TR_EXP_AVG_SQ (Adam's moment estimates). */
+enum nerf_train_state { NERF_TR_PARAMS = 0, NERF_TR_GRADS = 1, NERF_TR_EXP_AVG = 2, NERF_TR_EXP_AVG_SQ = 3 };
+int nerf_trainer_read(nerf_trainer* tr, int what, int net, float* const* host_out, int n_params);
+/* Overwrites one net's gradients (22 host tensors), e.g. to check clip + Adam on given grads. */
+int nerf_trainer_write_grads(nerf_trainer* tr, int net, const float* const* grads, int n_params);
+/* Clip + Adam + schedule on the gradients as they stand (the update half of train_step). */
+int nerf_trainer_update(nerf_trainer* tr, void* stream);
+/* The learning rate the next update uses (optimizer.param_groups[0]['lr']) and the steps taken. */
+double nerf_trainer_lr(const nerf_trainer* tr);
+long nerf_trainer_steps(const nerf_trainer* tr);
+
+/* Per-stage device time of the last train_step (HIP events on the step's stream, profiling on):
+ * 0 rays + sampling + encoding, 1 forward GEMMs, 2 colour head + volume render fwd/bwd,
+ * 3 backward GEMMs, 4 gradient reduction + clip + Adam + weight relayout. */
+#define NERF_TRAIN_N_STAGES 5
+int nerf_trainer_set_profiling(nerf_trainer* tr, int enable);
+int nerf_trainer_stage_ms(nerf_trainer* tr, float* ms_out /* [NERF_TRAIN_N_STAGES] */);
+/* Algorithmic fp32 FLOP of the last step's GEMMs (forward, backward-data, backward-weight,
+ * unpadded shapes), for roofline reporting. */
+double nerf_trainer_gemm_flops(const nerf_trainer* tr);
 
 #ifdef __cplusplus
 }

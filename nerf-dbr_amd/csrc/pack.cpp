@@ -251,3 +251,18 @@ extern "C" void nerf_uniform_z(const float* t_vals, int n, float near_, float fa
     z_out[i] = a + b;
   }
 }
+
+extern "C" void nerf_linspace01(int n, float* out) {
+  // torch.linspace(0, 1, n) on the CPU (ATen linspace_kernel): step = (1 - 0) / (n - 1)
+  // in fp32; the first half is start + step*i, the second end - step*(n-1-i), each a
+  // single rounding of the exact value (a fused multiply-add in ATen's build)
+  if (n <= 0) return;
+  if (n == 1) {
+    out[0] = 0.0f;
+    return;
+  }
+  const float step = 1.0f / float(n - 1);
+  const int half = n / 2;
+  for (int i = 0; i < n; ++i)
+    out[i] = i < half ? std::fma(step, float(i), 0.0f) : std::fma(-step, float(n - 1 - i), 1.0f);
+}

@@ -1,0 +1,1129 @@
+// NeRFTrainer.train_step on gfx950, fp32 throughout.
+//
+// Replaces src/training/trainer.py:83-138 (train_step) with _get_rays (:271-292),
+// _render_rays (:294-316), _query_network (:318-351), VolumeRenderer's stratified
+// sampling and volume_render (src/utils/rendering.py:17-52, 102-143), autograd,
+// clip_grad_norm_, optim.Adam and ExponentialLR.
+//
+// Structure of one step (both nets, one stream, no host synchronisation):
+//   rays of the selected pixels -> per net: samples + encodings -> 9 forward GEMMs
+//   (8 trunk layers, then the colour-0 layer and the density head as ONE GEMM of 129
+//   output columns: both read the trunk output) -> colour-1 + sigmoid -> volume render
+//   forward + MSE + its backward per ray -> head backward -> backward GEMMs (weight
+//   gradients as split-K partials over samples, data gradients with the ReLU mask in
+//   the epilogue) -> one reduction into the flat gradients -> grad norm, clip, Adam,
+//   and the relayout of the updated weights into the GEMM operand layouts.
+//
+// GEMM: C[M][N] = A[M][K] . B[K][N] on v_mfma_f32_32x32x2_f32 (exact fp32 fma chains),
+// 128x128 tiles per 256-thread workgroup, 16-deep k tiles double-buffered through LDS.
+// Activations are [sample][feature] row-major, so the three GEMM kinds are
+//   forward      A = X  [P][in]  (k contiguous)   B = W^T [in][out]
+//   backward-data A = dZ [P][out] (k contiguous)  B = W   [out][in]
+//   weight grad  A = dZ^T (m contiguous: dZ rows)  B = X   [P][in]   (K = samples, split)
+// and every B is [K][N] with n contiguous.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "nerf_device.h"
+#include "nerf_internal.h"
+
+namespace nerf {
+namespace {
+
+#define HIP_TRY(expr)                                                                                 \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) return set_error(NERF_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                           __FILE__, __LINE__);                                      \
+  } while (0)
+
+// ---------------------------------------------------------------- layouts --
+// Flat parameters of one NeRFModel in state-dict order (src/models/nerf.py:72-90):
+// layers.0..7 (weight [256][in], bias [256]), density_head ([1][256], [1]),
+// color_layers.0 ([128][283], [128]), color_layers.1 ([3][128], [3]).
+constexpr int kTrunkIn[8] = {63, 256, 256, 256, 319, 256, 256, 256};
+constexpr int kH = 256, kC0 = 128, kDirDim = 27;
+
+struct TensorDesc {
+  long off;
+  int rows, cols;
+};
+
+constexpr TensorDesc tensor_desc(int i) {
+  long off = 0;
+  for (int j = 0; j <= i; ++j) {
+    int rows = 0, cols = 1;
+    if (j < 16) {
+      rows = kH;
+      cols = (j % 2 == 0) ? kTrunkIn[j / 2] : 1;
+    } else if (j == 16) {
+      rows = 1, cols = kH;
+    } else if (j == 17) {
+      rows = 1;
+    } else if (j == 18) {
+      rows = kC0, cols = kH + kDirDim;
+    } else if (j == 19) {
+      rows = kC0;
+    } else if (j == 20) {
+      rows = 3, cols = kC0;
+    } else {
+      rows = 3;
+    }
+    if (j == i) return TensorDesc{off, rows, cols};
+    off += long(rows) * cols;
+  }
+  return TensorDesc{0, 0, 0};
+}
+constexpr long kNetFloats = tensor_desc(21).off + 3;   // 530,052
+static_assert(kNetFloats == 530052, "NeRFModel parameter count");
+constexpr long w_off(int l) { return tensor_desc(2 * l).off; }
+constexpr long b_off(int l) { return tensor_desc(2 * l + 1).off; }
+constexpr long kFDensW = tensor_desc(16).off, kFDensB = tensor_desc(17).off;
+constexpr long kFC0W = tensor_desc(18).off, kFC0B = tensor_desc(19).off;
+constexpr long kFC1W = tensor_desc(20).off, kFC1B = tensor_desc(21).off;
+
+constexpr int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// GEMM operand copies of one net's weights, rewritten after every update:
+//   Wt_l  [round16(in_l)][256]  trunk layer l transposed (forward B), zero rows past in_l
+//   WtH   [288][132]  head (colour-0 and density) transposed: column n < 128 = colour-0
+//                     row n, column 128 = density (zero for the direction inputs)
+//   W4h   [256][256]  layers.4 weight's hidden columns (backward-data B; the flat
+//                     tensor's 319-float rows are not 16-B aligned)
+//   WcH   [144][256]  head rows (colour-0 rows, then density) over the hidden inputs
+//   bH    [132]       head bias (colour-0, density, zeros)
+constexpr int kHeadN = kC0 + 1, kHeadLd = 132, kHeadK = kH + kDirDim;   // 129, 132, 283
+constexpr long wt_off(int l) {
+  long o = 0;
+  for (int j = 0; j < l; ++j) o += long(round_up(kTrunkIn[j], 16)) * kH;
+  return o;
+}
+constexpr long kWtH = wt_off(8);
+constexpr long kW4h = kWtH + long(round_up(kHeadK, 16)) * kHeadLd;
+constexpr long kWcH = kW4h + long(kH) * kH;
+constexpr long kBH = kWcH + 144L * kH;
+constexpr long kGemmFloats = round_up(int(kBH + kHeadLd), 64);
+
+// Per-sample activation workspace (floats per sample; each array [P][ld])
+constexpr int kPeLd = 64, kDpeLd = 28;
+
+constexpr int BM = 128, BN = 128, BK = 16, LDT = 132;   // LDS row stride (floats)
+
+// ------------------------------------------------------------------ GEMM --
+struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 % 4 == 0)
+  const float* p1 = nullptr;
+  const float* p2 = nullptr;
+  int ld1 = 0, ld2 = 0, w1 = 0x7fffffff;
+};
+
+enum Epi { kEpiBiasRelu = 0, kEpiMask = 1, kEpiPartial = 2 };
+
+struct GemmArgs {
+  int M = 0, N = 0, K = 0;
+  Src2 a, b;
+  float* c = nullptr;
+  int ldc = 0;
+  const float* bias = nullptr;      // kEpiBiasRelu: per column
+  const float* mask = nullptr;      // kEpiMask: C = acc where mask > 0, else 0
+  int ldm = 0;
+  float* bias_part = nullptr;       // kEpiPartial: [split][M] sums of A over the split's k
+  int k_split = 0;                  // kEpiPartial: k range per blockIdx.z (multiple of BK)
+  long c_split = 0;                 // kEpiPartial: floats per split partial
+};
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+
+// One thread's two float4 of a BMxBK A tile (rows m0.., k0..).  Sources hold at
+// least round_up4(width) valid floats per row; elements past M/K are zero.
+template <bool kAK>
+__device__ __forceinline__ void load_a(const GemmArgs& g, int m0, int k0, int t, f32x4 (&ra)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (kAK) {
+      const int m = m0 + (idx >> 2), k = k0 + 4 * (idx & 3);
+      if (m < g.M && k < g.K) {
+        v = k < g.a.w1 ? ld4(g.a.p1 + long(m) * g.a.ld1 + k) : ld4(g.a.p2 + long(m) * g.a.ld2 + (k - g.a.w1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (k + j >= g.K) v[j] = 0.0f;
+      }
+    } else {
+      const int k = k0 + (idx >> 5), m = m0 + 4 * (idx & 31);
+      if (k < g.K && m < g.M) {
+        v = ld4(g.a.p1 + long(k) * g.a.ld1 + m);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (m + j >= g.M) v[j] = 0.0f;
+      }
+    }
+    ra[i] = v;
+  }
+}
+
+template <bool kAK>
+__device__ __forceinline__ void store_a(float* as, int t, const f32x4 (&ra)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;
+    if (kAK) {
+      const int m = idx >> 2, q = idx & 3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) as[(4 * q + j) * LDT + m] = ra[i][j];
+    } else {
+      *(f32x4*)(as + (idx >> 5) * LDT + 4 * (idx & 31)) = ra[i];
+    }
+  }
+}
+
+__device__ __forceinline__ void load_b(const GemmArgs& g, int n0, int k0, int t, f32x4 (&rb)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;
+    const int k = k0 + (idx >> 5), n = n0 + 4 * (idx & 31);
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (k < g.K && n < g.N) {
+      v = n < g.b.w1 ? ld4(g.b.p1 + long(k) * g.b.ld1 + n) : ld4(g.b.p2 + long(k) * g.b.ld2 + (n - g.b.w1));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j >= g.N) v[j] = 0.0f;
+    }
+    rb[i] = v;
+  }
+}
+
+__device__ __forceinline__ void store_b(float* bs, int t, const f32x4 (&rb)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;
+    *(f32x4*)(bs + (idx >> 5) * LDT + 4 * (idx & 31)) = rb[i];
+  }
+}
+
+template <bool kAK, int kEpi>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+  __shared__ float As[2][BK * LDT];
+  __shared__ float Bs[2][BK * LDT];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
+  const int wm = w & 1, wn = w >> 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int kbeg = 0, kend = g.K;
+  if (kEpi == kEpiPartial) {
+    kbeg = blockIdx.z * g.k_split;
+    kend = min(g.K, kbeg + g.k_split);
+  }
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  float bsum = 0.0f;
+  f32x4 ra[2], rb[2];
+  if (nt > 0) {
+    load_a<kAK>(g, m0, kbeg, t, ra);
+    load_b(g, n0, kbeg, t, rb);
+    store_a<kAK>(As[0], t, ra);
+    store_b(Bs[0], t, rb);
+    __syncthreads();
+  }
+  for (int it = 0; it < nt; ++it) {
+    const int cur = it & 1;
+    const bool more = it + 1 < nt;
+    if (more) {
+      load_a<kAK>(g, m0, kbeg + (it + 1) * BK, t, ra);
+      load_b(g, n0, kbeg + (it + 1) * BK, t, rb);
+    }
+    const float* as = As[cur];
+    const float* bs = Bs[cur];
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int k = 2 * kk + h;
+      const float a0 = as[k * LDT + wm * 64 + l32], a1 = as[k * LDT + wm * 64 + 32 + l32];
+      const float b0 = bs[k * LDT + wn * 64 + l32], b1 = bs[k * LDT + wn * 64 + 32 + l32];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM) {
+#pragma unroll
+      for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, as[kr * LDT + t]);
+    }
+    if (more) {
+      store_a<kAK>(As[cur ^ 1], t, ra);
+      store_b(Bs[cur ^ 1], t, rb);
+    }
+    __syncthreads();
+  }
+  float* c = g.c + (kEpi == kEpiPartial ? long(blockIdx.z) * g.c_split : 0L);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + l32;
+      if (n >= g.N) continue;
+      const float bn = kEpi == kEpiBiasRelu ? g.bias[n] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
+        if (m >= g.M) continue;
+        float v = acc[i][j][r];
+        if (kEpi == kEpiBiasRelu) v = relu(__fadd_rn(v, bn));
+        if (kEpi == kEpiMask) v = g.mask[long(m) * g.ldm + n] > 0.0f ? v : 0.0f;
+        c[long(m) * g.ldc + n] = v;
+      }
+    }
+  if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM && m0 + t < g.M)
+    g.bias_part[long(blockIdx.z) * g.M + m0 + t] = bsum;
+}
+
+// ---------------------------------------------------------- element-wise --
+struct Pose {
+  float r[9];   // camera-to-world rotation, row-major
+  float t[3];
+};
+
+// _get_rays (trainer.py:271-292) for the selected pixels (:106-114), and their targets.
+__global__ void train_rays_kernel(Pose pose, int width, int n_pix, float half_w, float half_h, float focal,
+                                  const int* __restrict__ select, int n_rays, const float* __restrict__ image,
+                                  float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ target,
+                                  int* __restrict__ bad) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  int idx = select[r];
+  if (idx < 0 || idx >= n_pix) {
+    *bad = 1;
+    idx = 0;
+  }
+  const int row = idx / width, col = idx - (idx / width) * width;
+  const float dx = __fdiv_rn(__fsub_rn(float(col), half_w), focal);
+  const float dy = -__fdiv_rn(__fsub_rn(float(row), half_h), focal);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float p0 = __fmul_rn(dx, pose.r[3 * c + 0]);
+    const float p1 = __fmul_rn(dy, pose.r[3 * c + 1]);
+    const float p2 = -pose.r[3 * c + 2];
+    rays_d[3 * r + c] = __fadd_rn(__fadd_rn(p0, p1), p2);
+    rays_o[3 * r + c] = pose.t[c];
+    target[3 * r + c] = image[3L * idx + c];
+  }
+}
+
+// Sample points o + d*z and their encodings (nerf.py:24-45): pe [P][64] =
+// [x, sin/cos(2^k pi x) k < 10, 0], dpe [P][28] = [d, sin/cos(2^k pi d) k < 4, 0].
+__global__ void train_encode_kernel(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                                    const float* __restrict__ z, int z_stride, int n_samples, long n_points,
+                                    float* __restrict__ pe, float* __restrict__ dpe) {
+  const long p = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= n_points) return;
+  const long ray = p / n_samples;
+  const int s = int(p - ray * n_samples);
+  const float zz = z[ray * z_stride + s];
+  float x[3], d[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    d[c] = rays_d[3 * ray + c];
+    x[c] = sample_coord(rays_o[3 * ray + c], d[c], zz);
+  }
+  float v[kPeLd];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = x[c];
+#pragma unroll
+  for (int k = 0; k < 10; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) pe_sincos<false>(pe_coef(k), x[c], &v[3 + 6 * k + c], &v[6 + 6 * k + c]);
+  v[63] = 0.0f;
+  f32x4* po = (f32x4*)(pe + p * kPeLd);
+#pragma unroll
+  for (int q = 0; q < kPeLd / 4; ++q) po[q] = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+  float u[kDpeLd];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) u[c] = d[c];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) pe_sincos<false>(pe_coef(k), d[c], &u[3 + 6 * k + c], &u[6 + 6 * k + c]);
+  u[27] = 0.0f;
+  f32x4* du = (f32x4*)(dpe + p * kDpeLd);
+#pragma unroll
+  for (int q = 0; q < kDpeLd / 4; ++q) du[q] = f32x4{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]};
+}
+
+// colour-1 + sigmoid (nerf.py:123-129) per sample; the density is column 128 of
+// the head GEMM's output.  rgbs[p] = (r, g, b, sigma).
+__global__ void color_out_kernel(const float* __restrict__ hc, const float* __restrict__ prm, long n_points,
+                                 f32x4* __restrict__ rgbs) {
+  const long p = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= n_points) return;
+  const float* row = hc + p * kHeadLd;
+  const float* w1 = prm + kFC1W;
+  float acc[3] = {0.0f, 0.0f, 0.0f};
+  for (int j = 0; j < kC0; j += 4) {
+    const f32x4 v = ld4(row + j);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[c] = fmaf(v[q], w1[c * kC0 + j + q], acc[c]);
+  }
+  rgbs[p] = f32x4{sigmoid_ref(__fadd_rn(acc[0], prm[kFC1B])), sigmoid_ref(__fadd_rn(acc[1], prm[kFC1B + 1])),
+                  sigmoid_ref(__fadd_rn(acc[2], prm[kFC1B + 2])), row[kC0]};
+}
+
+// volume_render (rendering.py:102-143) forward, the MSE term of this ray, and the
+// backward of both (autograd's graph for these ops, restated):
+//   g_c          = 2 (rgb_map_c - target_c) / (3 n_rays)          (mse_loss backward)
+//   g_w_i        = sum_c g_c c_ic,  g_c_ic = w_i g_c                 (sum(w[...,None]*rgb))
+//   g_alpha_i    = g_w_i T_i - g_q_i,  g_T_i = g_w_i alpha_i         (w = alpha * T)
+//   g_q_j        = (sum_{i>=j} g_t_i t_i) / q_j,  g_t_i = g_T_{i+1}  (cumprod backward, the
+//                  reversed cumsum accumulated in double as torch's CPU cumsum)
+//   g_sigma_i    = g_alpha_i e_i dist_i [sigma_i > 0]                (alpha = 1 - exp(-relu(s) d))
+// then the sigmoid and density-ReLU backward: dpre[p] = (d r, d g, d b, d sigma) pre-activation.
+__global__ void render_train_kernel(const f32x4* __restrict__ rgbs, const float* __restrict__ z, int z_stride,
+                                    const float* __restrict__ rays_d, const float* __restrict__ target, int n_rays,
+                                    int n_samples, float gnorm, float* __restrict__ tbuf, f32x4* __restrict__ dpre,
+                                    float* __restrict__ loss_ray) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float dx = rays_d[3L * r], dy = rays_d[3L * r + 1], dz = rays_d[3L * r + 2];
+  const float norm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+  const float* zr = z + long(r) * z_stride;
+  const long base = long(r) * n_samples;
+  double tacc = 1.0;
+  float rm[3] = {0.0f, 0.0f, 0.0f};
+  for (int s = 0; s < n_samples; ++s) {
+    const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(zr[s + 1], zr[s]) : 1e10f, norm);
+    const f32x4 v = rgbs[base + s];
+    const float e = expf(__fmul_rn(-relu(v[3]), dist));
+    const float alpha = __fsub_rn(1.0f, e);
+    const float T = float(tacc);
+    const float w = __fmul_rn(alpha, T);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rm[c] = __fadd_rn(rm[c], __fmul_rn(w, v[c]));
+    tacc = __dmul_rn(tacc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
+    tbuf[base + s] = float(tacc);
+  }
+  float g[3], loss = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float diff = __fsub_rn(rm[c], target[3L * r + c]);
+    loss = __fadd_rn(loss, __fmul_rn(diff, diff));
+    g[c] = __fmul_rn(gnorm, diff);
+  }
+  loss_ray[r] = loss;
+  double suffix = 0.0;     // sum_{i >= s} g_t_i * t_i
+  float g_t = 0.0f;        // g_t_s = g_T_{s+1} (0 for the last sample)
+  for (int s = n_samples - 1; s >= 0; --s) {
+    const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(zr[s + 1], zr[s]) : 1e10f, norm);
+    const f32x4 v = rgbs[base + s];
+    const float sg = relu(v[3]);
+    const float e = expf(__fmul_rn(-sg, dist));
+    const float alpha = __fsub_rn(1.0f, e);
+    const float T = s > 0 ? tbuf[base + s - 1] : 1.0f;
+    const float t_s = tbuf[base + s];
+    const float q = __fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
+    const float w = __fmul_rn(alpha, T);
+    const float gw = __fadd_rn(__fadd_rn(__fmul_rn(g[0], v[0]), __fmul_rn(g[1], v[1])), __fmul_rn(g[2], v[2]));
+    suffix = __dadd_rn(suffix, double(__fmul_rn(t_s, g_t)));
+    const float g_q = __fdiv_rn(float(suffix), q);
+    const float g_alpha = __fsub_rn(__fmul_rn(gw, T), g_q);
+    const float g_sig = sg > 0.0f ? __fmul_rn(__fmul_rn(g_alpha, e), dist) : 0.0f;
+    g_t = __fmul_rn(gw, alpha);    // g_T_s = g_t_{s-1}
+    f32x4 d;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = __fmul_rn(__fmul_rn(__fmul_rn(w, g[c]), __fsub_rn(1.0f, v[c])), v[c]);
+    d[3] = g_sig;
+    dpre[base + s] = d;
+  }
+}
+
+// Backward of colour-1 and the colour-0 / density ReLUs: dhc [P][132] = the head
+// GEMM's pre-activation gradient (columns 0..127 colour-0, 128 density, then zeros).
+__global__ void head_bwd_kernel(const float* __restrict__ hc, const f32x4* __restrict__ dpre,
+                                const float* __restrict__ prm, long n_points, float* __restrict__ dhc) {
+  const long e = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= n_points * (kHeadLd / 4)) return;
+  const long p = e / (kHeadLd / 4);
+  const int n = int(e - p * (kHeadLd / 4)) * 4;
+  const f32x4 d = dpre[p];
+  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (n < kC0) {
+    const f32x4 hv = ld4(hc + p * kHeadLd + n);
+    const float* w1 = prm + kFC1W;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = __fadd_rn(__fadd_rn(__fmul_rn(d[0], w1[n + j]), __fmul_rn(d[1], w1[kC0 + n + j])),
+                                 __fmul_rn(d[2], w1[2 * kC0 + n + j]));
+      o[j] = hv[j] > 0.0f ? gj : 0.0f;
+    }
+  } else {
+    o[0] = d[3];
+  }
+  *(f32x4*)(dhc + p * kHeadLd + n) = o;
+}
+
+// --------------------------------------------------- gradient reduction --
+// Sums the split-K partials of one weight-gradient GEMM in split order and
+// scatters them into the flat gradients: rows [0, r1) to (w0 + m*ld0, n < nw0;
+// bias b0 + m), rows [r1, M) to (w1 + (m-r1)*ld1, n < nw1; bias b1 + m - r1).
+struct RedJob {
+  const float* part;
+  const float* bpart;
+  int splits, M, N;
+  int r1;
+  long w0, b0;
+  int ld0, nw0;
+  long w1, b1;
+  int ld1, nw1;
+};
+constexpr int kMaxJobs = 11;
+struct RedJobs {
+  RedJob j[kMaxJobs];
+};
+
+__global__ void reduce_grads_kernel(RedJobs jobs, float* __restrict__ grads) {
+  const RedJob& jb = jobs.j[blockIdx.y];
+  const long e = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long mn = long(jb.M) * jb.N;
+  if (e < mn) {
+    const int m = int(e / jb.N), n = int(e - long(m) * jb.N);
+    const bool g0 = m < jb.r1;
+    if (n >= (g0 ? jb.nw0 : jb.nw1)) return;
+    float s = 0.0f;
+    for (int k = 0; k < jb.splits; ++k) s = __fadd_rn(s, jb.part[k * mn + e]);
+    grads[g0 ? jb.w0 + long(m) * jb.ld0 + n : jb.w1 + long(m - jb.r1) * jb.ld1 + n] = s;
+  } else if (e < mn + jb.M) {
+    const int m = int(e - mn);
+    float s = 0.0f;
+    for (int k = 0; k < jb.splits; ++k) s = __fadd_rn(s, jb.bpart[long(k) * jb.M + m]);
+    grads[m < jb.r1 ? jb.b0 + m : jb.b1 + (m - jb.r1)] = s;
+  }
+}
+
+// Sum of squares of all gradients (double), per block.
+__global__ void sumsq_kernel(const float* __restrict__ g, long n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long i = long(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += long(gridDim.x) * blockDim.x) {
+    const double v = g[i];
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (int(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// Loss (trainer.py:117-119: mean over [n_rays][3] per net, summed) and the clip
+// coefficient of clip_grad_norm_: min(max_norm / (total_norm + 1e-6), 1).
+// out: [0] loss, [1] coarse MSE, [2] fine MSE; coef: the factor Adam applies.
+__global__ void finalize_kernel(const float* __restrict__ loss_ray, int n_rays, const double* __restrict__ sq_part,
+                                int n_part, float max_norm, float* __restrict__ out, float* __restrict__ coef) {
+  __shared__ double red[3][256];
+  double a = 0.0, b = 0.0, q = 0.0;
+  for (int i = threadIdx.x; i < n_rays; i += blockDim.x) {
+    a += loss_ray[i];
+    b += loss_ray[n_rays + i];
+  }
+  if (sq_part)
+    for (int i = threadIdx.x; i < n_part; i += blockDim.x) q += sq_part[i];
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  red[2][threadIdx.x] = q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (int(threadIdx.x) < o)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float denom = float(3.0 * n_rays);
+    const float mc = __fdiv_rn(float(red[0][0]), denom), mf = __fdiv_rn(float(red[1][0]), denom);
+    if (out) {
+      out[0] = __fadd_rn(mc, mf);
+      out[1] = mc;
+      out[2] = mf;
+    }
+    if (coef) {
+      float c = 1.0f;
+      if (sq_part && max_norm > 0.0f) {
+        const float total = float(sqrt(red[2][0]));
+        c = fminf(__fdiv_rn(max_norm, __fadd_rn(total, 1e-6f)), 1.0f);
+      }
+      *coef = c;
+    }
+  }
+}
+
+// torch.optim.Adam, single-tensor form (torch/optim/adam.py), after clip_grad_norm_'s
+// in-place scaling: g *= coef; g += wd * p; m = lerp(m, g, 1 - b1); v = v*b2 + (1-b2)*g*g;
+// p += (-step_size * m) / (sqrt(v) / bc2_sqrt + eps).
+struct AdamArgs {
+  float one_minus_b1, b2, one_minus_b2, wd, neg_step_size, bc2_sqrt, eps;
+};
+__global__ void adam_kernel(float* __restrict__ p, float* __restrict__ grad, float* __restrict__ m,
+                            float* __restrict__ v, long n, const float* __restrict__ coef, AdamArgs a) {
+  const long i = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float g = __fmul_rn(grad[i], *coef);
+  grad[i] = g;                       // the reference's param.grad after the step: the clipped gradient
+  const float pv = p[i];
+  if (a.wd != 0.0f) g = fmaf(pv, a.wd, g);
+  const float mv = fmaf(a.one_minus_b1, __fsub_rn(g, m[i]), m[i]);
+  const float vv = __fadd_rn(__fmul_rn(v[i], a.b2), __fmul_rn(__fmul_rn(a.one_minus_b2, g), g));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), a.bc2_sqrt), a.eps);
+  p[i] = __fadd_rn(pv, __fdiv_rn(__fmul_rn(a.neg_step_size, mv), denom));
+  m[i] = mv;
+  v[i] = vv;
+}
+
+// Flat parameters -> the GEMM operand copies (layout above), both nets.
+__global__ void relayout_kernel(const float* __restrict__ params, float* __restrict__ gemmw) {
+  const long e = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= kGemmFloats) return;
+  const float* prm = params + blockIdx.y * kNetFloats;
+  float* out = gemmw + blockIdx.y * kGemmFloats;
+  float v = 0.0f;
+  if (e < kWtH) {
+    int l = 0;
+    while (l < 7 && e >= wt_off(l + 1)) ++l;
+    const long o = e - wt_off(l);
+    const int k = int(o / kH), n = int(o - long(k) * kH);
+    if (k < kTrunkIn[l]) v = prm[w_off(l) + long(n) * kTrunkIn[l] + k];
+  } else if (e < kW4h) {
+    const long o = e - kWtH;
+    const int k = int(o / kHeadLd), n = int(o - long(k) * kHeadLd);
+    if (k < kHeadK && n < kC0) v = prm[kFC0W + long(n) * kHeadK + k];
+    else if (k < kH && n == kC0) v = prm[kFDensW + k];
+  } else if (e < kWcH) {
+    const long o = e - kW4h;
+    const int n = int(o / kH), k = int(o - long(n) * kH);
+    v = prm[w_off(4) + long(n) * kTrunkIn[4] + k];
+  } else if (e < kBH) {
+    const long o = e - kWcH;
+    const int n = int(o / kH), k = int(o - long(n) * kH);
+    if (n < kC0) v = prm[kFC0W + long(n) * kHeadK + k];
+    else if (n == kC0) v = prm[kFDensW + k];
+  } else if (e < kBH + kHeadLd) {
+    const int n = int(e - kBH);
+    if (n < kC0) v = prm[kFC0B + n];
+    else if (n == kC0) v = prm[kFDensB];
+  }
+  out[e] = v;
+}
+
+inline unsigned blocks_for(long n, int per) { return unsigned((n + per - 1) / per); }
+
+}  // namespace
+}  // namespace nerf
+
+using namespace nerf;
+
+// ----------------------------------------------------------------- host --
+struct nerf_trainer {
+  int device = 0;
+  nerf_train_config cfg{};
+  double lr = 0.0;
+  long steps = 0;
+  float* params = nullptr;   // [2][kNetFloats]
+  float* grads = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  float* gemmw = nullptr;    // [2][kGemmFloats]
+  float* ztab = nullptr;     // coarse table [n_coarse], fine table [n_fine]
+  float* scal = nullptr;     // [0] clip coefficient, then double sum-of-squares partials
+  int* bad = nullptr;        // device flag: a select index out of range
+  float* ws = nullptr;       // per-step workspace
+  size_t ws_cap = 0;
+  float* part = nullptr;     // weight-gradient partials (one net at a time)
+  size_t part_cap = 0;
+  bool profiling = false;
+  bool have_times = false;
+  hipEvent_t ev[12] = {};
+  double gemm_flops = 0.0;
+};
+
+namespace {
+
+constexpr int kSqBlocks = 256;
+
+struct DeviceGuardT {
+  int prev = -1;
+  explicit DeviceGuardT(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceGuardT() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int grow_buf(float*& p, size_t& cap, size_t need, const char* what) {
+  if (need <= cap) return NERF_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  const size_t n = need + need / 8;
+  hipError_t e = hipMalloc((void**)&p, n * sizeof(float));
+  if (e != hipSuccess) return set_error(NERF_E_HIP, "hipMalloc %s (%zu bytes): %s", what, n * sizeof(float), hipGetErrorString(e));
+  cap = n;
+  return NERF_OK;
+}
+
+inline size_t al64(size_t x) { return (x + 63) / 64 * 64; }
+
+// Per-net activation arrays inside the workspace.
+struct Acts {
+  float *pe, *dpe, *h[8], *hc, *rgbs, *dpre, *tb, *dhc, *d0, *d1;
+};
+
+size_t acts_floats(long P) {
+  const size_t p = size_t(P);
+  return al64(p * kPeLd) + al64(p * kDpeLd) + 8 * al64(p * kH) + al64(p * kHeadLd) + 2 * al64(p * 4) + al64(p) +
+         al64(p * kHeadLd) + 2 * al64(p * kH);
+}
+
+size_t head_floats(int n_rays, int n_coarse) {
+  return al64(size_t(n_rays) * 9) + al64(size_t(n_rays) * n_coarse) + al64(size_t(n_rays) * 2);
+}
+
+Acts carve_acts(float* base, long P) {
+  const size_t p = size_t(P);
+  Acts a;
+  float* q = base;
+  auto take = [&](size_t n) {
+    float* r = q;
+    q += al64(n);
+    return r;
+  };
+  a.pe = take(p * kPeLd);
+  a.dpe = take(p * kDpeLd);
+  for (auto& hh : a.h) hh = take(p * kH);
+  a.hc = take(p * kHeadLd);
+  a.rgbs = take(p * 4);
+  a.dpre = take(p * 4);
+  a.tb = take(p);
+  a.dhc = take(p * kHeadLd);
+  a.d0 = take(p * kH);
+  a.d1 = take(p * kH);
+  return a;
+}
+
+template <bool kAK, int kEpi>
+hipError_t gemm(const GemmArgs& g, int splits, hipStream_t s) {
+  const dim3 grid{blocks_for(g.M, BM), blocks_for(g.N, BN), unsigned(kEpi == kEpiPartial ? splits : 1)};
+  hipLaunchKernelGGL((gemm_f32_kernel<kAK, kEpi>), grid, dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+// Weight-gradient GEMM job: k split over the samples so that the grid fills the chip.
+struct WJob {
+  int M, N;
+  int splits, k_split;
+  size_t off, boff;   // partial and bias-partial offsets in the part buffer
+};
+
+WJob plan_wjob(int M, int N, long P, size_t& cursor) {
+  WJob j{M, N, 1, 0, 0, 0};
+  const int tiles = int(blocks_for(M, BM) * blocks_for(N, BN));
+  const int ktiles = int(blocks_for(P, BK));
+  const int target = 2 * current_device_cus();
+  int splits = std::max(1, std::min(target / tiles, std::max(1, ktiles / 4)));
+  j.k_split = int(blocks_for(ktiles, splits)) * BK;
+  j.splits = int(blocks_for(P, j.k_split));
+  j.off = cursor;
+  cursor += al64(size_t(j.splits) * M * N);
+  j.boff = cursor;
+  cursor += al64(size_t(j.splits) * M);
+  return j;
+}
+
+double gemm_macs_per_sample() {
+  double fwd = 0.0;
+  for (int l = 0; l < 8; ++l) fwd += double(kTrunkIn[l]) * kH;
+  fwd += double(kHeadK) * kC0 + kH;                       // colour-0 + density
+  const double bwd_data = 7.0 * kH * kH + double(kC0 + 1) * kH;
+  return 2.0 * fwd + bwd_data;                            // forward, weight grads, data grads
+}
+
+// Forward + backward of one net on P = n_rays * S samples; gradients into grads (flat).
+int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d, const float* target,
+             const float* z, int z_stride, int n_rays, int S, float* loss_ray, hipStream_t s, int ev0) {
+  const long P = long(n_rays) * S;
+  Acts a = carve_acts(tr->ws + head_floats(n_rays, tr->cfg.n_coarse), P);
+  const float* prm = tr->params + net * kNetFloats;
+  const float* gw = tr->gemmw + net * kGemmFloats;
+  float* grads = tr->grads + net * kNetFloats;
+  auto mark = [&](int i) -> int {
+    if (tr->profiling) HIP_TRY(hipEventRecord(tr->ev[ev0 + i], s));
+    return NERF_OK;
+  };
+  int rc;
+  hipLaunchKernelGGL(train_encode_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, rays_o, rays_d, z, z_stride, S,
+                     P, a.pe, a.dpe);
+  HIP_TRY(hipGetLastError());
+  if ((rc = mark(1)) != NERF_OK) return rc;
+
+  // forward (nerf.py:104-121)
+  for (int l = 0; l < 8; ++l) {
+    GemmArgs g;
+    g.M = int(P), g.N = kH, g.K = kTrunkIn[l];
+    if (l == 0) g.a = Src2{a.pe, nullptr, kPeLd, 0, 0x7fffffff};
+    else if (l == 4) g.a = Src2{a.h[3], a.pe, kH, kPeLd, kH};
+    else g.a = Src2{a.h[l - 1], nullptr, kH, 0, 0x7fffffff};
+    g.b = Src2{gw + wt_off(l), nullptr, kH, 0, 0x7fffffff};
+    g.c = a.h[l], g.ldc = kH;
+    g.bias = prm + b_off(l);
+    HIP_TRY((gemm<true, kEpiBiasRelu>(g, 1, s)));
+  }
+  {
+    GemmArgs g;
+    g.M = int(P), g.N = kHeadN, g.K = kHeadK;
+    g.a = Src2{a.h[7], a.dpe, kH, kDpeLd, kH};
+    g.b = Src2{gw + kWtH, nullptr, kHeadLd, 0, 0x7fffffff};
+    g.c = a.hc, g.ldc = kHeadLd;
+    g.bias = gw + kBH;
+    HIP_TRY((gemm<true, kEpiBiasRelu>(g, 1, s)));
+  }
+  if ((rc = mark(2)) != NERF_OK) return rc;
+
+  // colour head, volume render + loss, their backward (rendering.py:102-143, trainer.py:117-126)
+  hipLaunchKernelGGL(color_out_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, a.hc, prm, P, (f32x4*)a.rgbs);
+  HIP_TRY(hipGetLastError());
+  const float gnorm = float(2.0 / (3.0 * n_rays));
+  hipLaunchKernelGGL(render_train_kernel, dim3(blocks_for(n_rays, 64)), dim3(64), 0, s, (const f32x4*)a.rgbs, z,
+                     z_stride, rays_d, target, n_rays, S, gnorm, a.tb, (f32x4*)a.dpre, loss_ray);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks_for(P * (kHeadLd / 4), 256)), dim3(256), 0, s, a.hc,
+                     (const f32x4*)a.dpre, prm, P, a.dhc);
+  HIP_TRY(hipGetLastError());
+  if ((rc = mark(3)) != NERF_OK) return rc;
+
+  // backward GEMMs; weight gradients as split partials
+  size_t cur = 0;
+  WJob jc1 = plan_wjob(3, kC0, P, cur);
+  WJob jh = plan_wjob(kHeadN, kHeadK, P, cur);
+  WJob jl[8];
+  for (int l = 7; l >= 0; --l) jl[l] = plan_wjob(kH, kTrunkIn[l], P, cur);
+  if ((rc = grow_buf(tr->part, tr->part_cap, cur, "gradient partials")) != NERF_OK) return rc;
+  auto wgrad = [&](const WJob& j, const float* A, int lda, Src2 B) -> hipError_t {
+    GemmArgs g;
+    g.M = j.M, g.N = j.N, g.K = int(P);
+    g.a = Src2{A, nullptr, lda, 0, 0x7fffffff};
+    g.b = B;
+    g.c = tr->part + j.off, g.ldc = j.N;
+    g.bias_part = tr->part + j.boff;
+    g.k_split = j.k_split;
+    g.c_split = long(j.M) * j.N;
+    return gemm<false, kEpiPartial>(g, j.splits, s);
+  };
+  HIP_TRY(wgrad(jc1, a.dpre, 4, Src2{a.hc, nullptr, kHeadLd, 0, 0x7fffffff}));
+  HIP_TRY(wgrad(jh, a.dhc, kHeadLd, Src2{a.h[7], a.dpe, kH, kDpeLd, kH}));
+  {
+    GemmArgs g;   // d h7 = dhc . [colour-0 rows; density row] over the hidden inputs, ReLU mask of h7
+    g.M = int(P), g.N = kH, g.K = kHeadN;
+    g.a = Src2{a.dhc, nullptr, kHeadLd, 0, 0x7fffffff};
+    g.b = Src2{gw + kWcH, nullptr, kH, 0, 0x7fffffff};
+    g.c = a.d0, g.ldc = kH;
+    g.mask = a.h[7], g.ldm = kH;
+    HIP_TRY((gemm<true, kEpiMask>(g, 1, s)));
+  }
+  float* dz = a.d0;
+  float* dn = a.d1;
+  for (int l = 7; l >= 0; --l) {
+    Src2 X;
+    if (l == 0) X = Src2{a.pe, nullptr, kPeLd, 0, 0x7fffffff};
+    else if (l == 4) X = Src2{a.h[3], a.pe, kH, kPeLd, kH};
+    else X = Src2{a.h[l - 1], nullptr, kH, 0, 0x7fffffff};
+    HIP_TRY(wgrad(jl[l], dz, kH, X));
+    if (l == 0) break;
+    GemmArgs g;
+    g.M = int(P), g.N = kH, g.K = kH;
+    g.a = Src2{dz, nullptr, kH, 0, 0x7fffffff};
+    g.b = l == 4 ? Src2{gw + kW4h, nullptr, kH, 0, 0x7fffffff} : Src2{prm + w_off(l), nullptr, kH, 0, 0x7fffffff};
+    g.c = dn, g.ldc = kH;
+    g.mask = a.h[l - 1], g.ldm = kH;
+    HIP_TRY((gemm<true, kEpiMask>(g, 1, s)));
+    std::swap(dz, dn);
+  }
+  if ((rc = mark(4)) != NERF_OK) return rc;
+
+  // partials -> flat gradients
+  RedJobs jobs{};
+  auto job = [&](int i, const WJob& j, int r1, long w0, long b0, int ld0, int nw0, long w1, long b1, int ld1,
+                 int nw1) {
+    jobs.j[i] = RedJob{tr->part + j.off, tr->part + j.boff, j.splits, j.M, j.N, r1, w0, b0, ld0, nw0, w1, b1, ld1, nw1};
+  };
+  long maxe = 0;
+  for (int l = 0; l < 8; ++l) {
+    job(l, jl[l], kH, w_off(l), b_off(l), kTrunkIn[l], kTrunkIn[l], 0, 0, 0, 0);
+    maxe = std::max(maxe, long(jl[l].M) * jl[l].N + jl[l].M);
+  }
+  job(8, jh, kC0, kFC0W, kFC0B, kHeadK, kHeadK, kFDensW, kFDensB, kH, kH);
+  job(9, jc1, 3, kFC1W, kFC1B, kC0, kC0, 0, 0, 0, 0);
+  maxe = std::max(maxe, long(jh.M) * jh.N + jh.M);
+  hipLaunchKernelGGL(reduce_grads_kernel, dim3(blocks_for(maxe, 256), 10), dim3(256), 0, s, jobs, grads);
+  HIP_TRY(hipGetLastError());
+  tr->gemm_flops += 2.0 * gemm_macs_per_sample() * double(P);
+  return NERF_OK;
+}
+
+int update_impl(nerf_trainer* tr, hipStream_t s) {
+  double* sq = (double*)(tr->scal + 4);
+  const long n = 2 * kNetFloats;
+  const bool clip = tr->cfg.grad_clip > 0.0;
+  if (clip) {
+    hipLaunchKernelGGL(sumsq_kernel, dim3(kSqBlocks), dim3(256), 0, s, tr->grads, n, sq);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)nullptr, 0,
+                     clip ? (const double*)sq : (const double*)nullptr, kSqBlocks, float(tr->cfg.grad_clip),
+                     (float*)nullptr, tr->scal);
+  HIP_TRY(hipGetLastError());
+  // torch.optim.Adam step scalars (adam.py, _single_tensor_adam): python floats
+  const double step = double(tr->steps + 1);
+  const double bc1 = 1.0 - std::pow(tr->cfg.beta1, step);
+  const double bc2 = 1.0 - std::pow(tr->cfg.beta2, step);
+  AdamArgs aa;
+  aa.one_minus_b1 = float(1.0 - tr->cfg.beta1);
+  aa.b2 = float(tr->cfg.beta2);
+  aa.one_minus_b2 = float(1.0 - tr->cfg.beta2);
+  aa.wd = float(tr->cfg.weight_decay);
+  aa.neg_step_size = float(-(tr->lr / bc1));
+  aa.bc2_sqrt = float(std::pow(bc2, 0.5));
+  aa.eps = float(tr->cfg.eps);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, tr->params, tr->grads, tr->m, tr->v, n,
+                     (const float*)tr->scal, aa);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, s, (const float*)tr->params,
+                     tr->gemmw);
+  HIP_TRY(hipGetLastError());
+  tr->steps += 1;
+  tr->lr = tr->lr * tr->cfg.lr_gamma;   // ExponentialLR.step: lr * gamma
+  return NERF_OK;
+}
+
+size_t param_offset(int i) { return size_t(tensor_desc(i).off); }
+size_t param_count(int i) { return size_t(tensor_desc(i).rows) * size_t(tensor_desc(i).cols); }
+
+}  // namespace
+
+extern "C" {
+
+int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* const* coarse,
+                        const float* const* fine, int n_params, nerf_trainer** out) {
+  if (!out) return set_error(NERF_E_INVALID, "null out pointer");
+  *out = nullptr;
+  if (!cfg || !coarse || !fine) return set_error(NERF_E_INVALID, "nerf_trainer_create: null argument");
+  if (n_params != NERF_N_PARAMS) return set_error(NERF_E_INVALID, "expected %d parameter tensors, got %d", NERF_N_PARAMS, n_params);
+  if (cfg->n_coarse < 2 || cfg->n_coarse > 1024 || cfg->n_fine < 2 || cfg->n_fine > 1024)
+    return set_error(NERF_E_INVALID, "nerf_trainer_create: sample counts %d / %d (2..1024)", cfg->n_coarse, cfg->n_fine);
+  if (!(cfg->lr >= 0.0) || !(cfg->beta1 >= 0.0 && cfg->beta1 < 1.0) || !(cfg->beta2 >= 0.0 && cfg->beta2 < 1.0) ||
+      !(cfg->eps >= 0.0) || !(cfg->weight_decay >= 0.0))
+    return set_error(NERF_E_INVALID, "nerf_trainer_create: bad optimizer settings");
+  for (int i = 0; i < NERF_N_PARAMS; ++i)
+    if (!coarse[i] || !fine[i]) return set_error(NERF_E_INVALID, "nerf_trainer_create: null tensor %d", i);
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd)
+    return set_error(NERF_E_NO_DEVICE, "no HIP device %d (count %d)", device, nd);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_error(NERF_E_NO_DEVICE, "device %d is %s; this library is built for gfx950 (MI355X)", device,
+                     prop.gcnArchName);
+  DeviceGuardT dg(device);
+  nerf_trainer* tr = new nerf_trainer();
+  tr->device = device;
+  tr->cfg = *cfg;
+  tr->lr = cfg->lr;
+  auto fail = [&](int rc) {
+    nerf_trainer_destroy(tr);
+    return rc;
+  };
+  const size_t bytes = sizeof(float) * 2 * kNetFloats;
+  for (float** p : {&tr->params, &tr->grads, &tr->m, &tr->v})
+    if (hipMalloc((void**)p, bytes) != hipSuccess) return fail(set_error(NERF_E_HIP, "hipMalloc trainer state"));
+  if (hipMalloc((void**)&tr->gemmw, sizeof(float) * 2 * kGemmFloats) != hipSuccess ||
+      hipMalloc((void**)&tr->ztab, sizeof(float) * 2048) != hipSuccess ||
+      hipMalloc((void**)&tr->scal, sizeof(float) * (4 + 2 * kSqBlocks)) != hipSuccess ||
+      hipMalloc((void**)&tr->bad, sizeof(int)) != hipSuccess)
+    return fail(set_error(NERF_E_HIP, "hipMalloc trainer buffers"));
+  std::vector<float> host(2 * kNetFloats);
+  for (int net = 0; net < 2; ++net) {
+    const float* const* src = net ? fine : coarse;
+    for (int i = 0; i < NERF_N_PARAMS; ++i)
+      std::memcpy(host.data() + net * kNetFloats + param_offset(i), src[i], sizeof(float) * param_count(i));
+  }
+  if (hipMemcpy(tr->params, host.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(tr->grads, 0, bytes) != hipSuccess || hipMemset(tr->m, 0, bytes) != hipSuccess ||
+      hipMemset(tr->v, 0, bytes) != hipSuccess || hipMemset(tr->bad, 0, sizeof(int)) != hipSuccess)
+    return fail(set_error(NERF_E_HIP, "trainer upload failed"));
+  // uniform depth tables z = near*(1-t) + far*t over torch.linspace(0, 1, n)
+  // (rendering.py:37-38): t is computed here as torch's CPU linspace does for
+  // these sizes (checked against torch by tests/test_host_layout.py)
+  std::vector<float> zt(2048, 0.0f), tv;
+  for (int net = 0; net < 2; ++net) {
+    const int n = net ? cfg->n_fine : cfg->n_coarse;
+    tv.assign(n, 0.0f);
+    nerf_linspace01(n, tv.data());
+    nerf_uniform_z(tv.data(), n, cfg->near_, cfg->far_, zt.data() + 1024 * net);
+  }
+  if (hipMemcpy(tr->ztab, zt.data(), sizeof(float) * 2048, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_error(NERF_E_HIP, "trainer z upload failed"));
+  for (auto& e : tr->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(set_error(NERF_E_HIP, "hipEventCreate"));
+  hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, 0, (const float*)tr->params,
+                     tr->gemmw);
+  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return fail(set_error(NERF_E_HIP, "trainer relayout failed"));
+  *out = tr;
+  return NERF_OK;
+}
+
+void nerf_trainer_destroy(nerf_trainer* tr) {
+  if (!tr) return;
+  DeviceGuardT dg(tr->device);
+  (void)hipDeviceSynchronize();
+  for (float* p : {tr->params, tr->grads, tr->m, tr->v, tr->gemmw, tr->ztab, tr->scal, tr->ws, tr->part})
+    if (p) (void)hipFree(p);
+  if (tr->bad) (void)hipFree(tr->bad);
+  for (auto& e : tr->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete tr;
+}
+
+int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width, float focal, const float* c2w,
+                    const int32_t* select, int n_rays, const float* t_rand, int flags, float* loss_out, void* stream) {
+  if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  if (!image || !c2w || !select || !t_rand) return set_error(NERF_E_INVALID, "nerf_train_step: null argument");
+  if (height <= 0 || width <= 0 || n_rays <= 0 || long(height) * width > 0x7fffffffL)
+    return set_error(NERF_E_INVALID, "nerf_train_step: bad sizes %dx%d, %d rays", height, width, n_rays);
+  if (!(focal > 0.0f)) return set_error(NERF_E_INVALID, "nerf_train_step: focal must be positive");
+  const int Smax = std::max(tr->cfg.n_coarse, tr->cfg.n_fine);
+  if (long(n_rays) * Smax > 0x7fffffffL / 2) return set_error(NERF_E_INVALID, "nerf_train_step: too many samples");
+  DeviceGuardT dg(tr->device);
+  hipStream_t s = (hipStream_t)stream;
+  const long Pmax = long(n_rays) * Smax;
+  // workspace: rays_o, rays_d, targets [n_rays][3] each | coarse z [n_rays][n_coarse] |
+  // per-ray squared errors [2][n_rays] | one net's activations (net_pass)
+  const size_t head = head_floats(n_rays, tr->cfg.n_coarse);
+  int rc;
+  if ((rc = grow_buf(tr->ws, tr->ws_cap, head + acts_floats(Pmax) + 64, "training workspace")) != NERF_OK) return rc;
+  float* rays_o = tr->ws;
+  float* rays_d = rays_o + 3 * size_t(n_rays);
+  float* target = rays_d + 3 * size_t(n_rays);
+  float* zc = tr->ws + al64(size_t(n_rays) * 9);
+  float* loss_ray = zc + al64(size_t(n_rays) * tr->cfg.n_coarse);
+  tr->have_times = false;
+  tr->gemm_flops = 0.0;
+  auto mark = [&](int i) -> int {
+    if (tr->profiling) HIP_TRY(hipEventRecord(tr->ev[i], s));
+    return NERF_OK;
+  };
+  if ((rc = mark(0)) != NERF_OK) return rc;
+  Pose pose;
+  for (int c = 0; c < 3; ++c) {
+    for (int j = 0; j < 3; ++j) pose.r[3 * c + j] = c2w[4 * c + j];
+    pose.t[c] = c2w[4 * c + 3];
+  }
+  hipLaunchKernelGGL(train_rays_kernel, dim3(blocks_for(n_rays, 256)), dim3(256), 0, s, pose, width, height * width,
+                     float(width * 0.5), float(height * 0.5), focal, (const int*)select, n_rays, image, rays_o, rays_d,
+                     target, tr->bad);
+  HIP_TRY(hipGetLastError());
+  // coarse samples stratified with the injected draw (rendering.py:42-47)
+  HIP_TRY(launch_sample(tr->ztab, t_rand, n_rays, tr->cfg.n_coarse, nullptr, nullptr, zc, nullptr, s));
+  if ((rc = net_pass(tr, 0, rays_o, rays_d, target, zc, tr->cfg.n_coarse, n_rays, tr->cfg.n_coarse, loss_ray, s, 0)) !=
+      NERF_OK)
+    return rc;
+  if ((rc = mark(5)) != NERF_OK) return rc;
+  if ((rc = net_pass(tr, 1, rays_o, rays_d, target, tr->ztab + 1024, 0, n_rays, tr->cfg.n_fine, loss_ray + n_rays, s,
+                     5)) != NERF_OK)
+    return rc;
+  if ((rc = mark(10)) != NERF_OK) return rc;
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)loss_ray, n_rays, (const double*)nullptr,
+                     0, 0.0f, loss_out, (float*)nullptr);
+  HIP_TRY(hipGetLastError());
+  if (!(flags & NERF_TRAIN_NO_UPDATE) && (rc = update_impl(tr, s)) != NERF_OK) return rc;
+  if ((rc = mark(11)) != NERF_OK) return rc;
+  tr->have_times = tr->profiling;
+  return NERF_OK;
+}
+
+int nerf_trainer_update(nerf_trainer* tr, void* stream) {
+  if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  DeviceGuardT dg(tr->device);
+  return update_impl(tr, (hipStream_t)stream);
+}
+
+int nerf_trainer_read(nerf_trainer* tr, int what, int net, float* const* host_out, int n_params) {
+  if (!tr || !host_out) return set_error(NERF_E_INVALID, "nerf_trainer_read: null argument");
+  if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
+  if (n_params != NERF_N_PARAMS) return set_error(NERF_E_INVALID, "expected %d tensors", NERF_N_PARAMS);
+  const float* src = what == NERF_TR_PARAMS ? tr->params : what == NERF_TR_GRADS ? tr->grads
+                   : what == NERF_TR_EXP_AVG ? tr->m : what == NERF_TR_EXP_AVG_SQ ? tr->v : nullptr;
+  if (!src) return set_error(NERF_E_INVALID, "nerf_trainer_read: bad state %d", what);
+  DeviceGuardT dg(tr->device);
+  HIP_TRY(hipDeviceSynchronize());
+  int bad = 0;
+  HIP_TRY(hipMemcpy(&bad, tr->bad, sizeof(int), hipMemcpyDeviceToHost));
+  if (bad) return set_error(NERF_E_INVALID, "a train_step's select held an index outside the image");
+  std::vector<float> host(kNetFloats);
+  HIP_TRY(hipMemcpy(host.data(), src + net * kNetFloats, sizeof(float) * kNetFloats, hipMemcpyDeviceToHost));
+  for (int i = 0; i < NERF_N_PARAMS; ++i) {
+    if (!host_out[i]) return set_error(NERF_E_INVALID, "nerf_trainer_read: null buffer %d", i);
+    std::memcpy(host_out[i], host.data() + param_offset(i), sizeof(float) * param_count(i));
+  }
+  return NERF_OK;
+}
+
+int nerf_trainer_write_grads(nerf_trainer* tr, int net, const float* const* grads, int n_params) {
+  if (!tr || !grads) return set_error(NERF_E_INVALID, "nerf_trainer_write_grads: null argument");
+  if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
+  if (n_params != NERF_N_PARAMS) return set_error(NERF_E_INVALID, "expected %d tensors", NERF_N_PARAMS);
+  std::vector<float> host(kNetFloats);
+  for (int i = 0; i < NERF_N_PARAMS; ++i) {
+    if (!grads[i]) return set_error(NERF_E_INVALID, "nerf_trainer_write_grads: null tensor %d", i);
+    std::memcpy(host.data() + param_offset(i), grads[i], sizeof(float) * param_count(i));
+  }
+  DeviceGuardT dg(tr->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(tr->grads + net * kNetFloats, host.data(), sizeof(float) * kNetFloats, hipMemcpyHostToDevice));
+  return NERF_OK;
+}
+
+double nerf_trainer_lr(const nerf_trainer* tr) { return tr ? tr->lr : 0.0; }
+long nerf_trainer_steps(const nerf_trainer* tr) { return tr ? tr->steps : 0; }
+double nerf_trainer_gemm_flops(const nerf_trainer* tr) { return tr ? tr->gemm_flops : 0.0; }
+
+int nerf_trainer_set_profiling(nerf_trainer* tr, int enable) {
+  if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  tr->profiling = enable != 0;
+  return NERF_OK;
+}
+
+int nerf_trainer_stage_ms(nerf_trainer* tr, float* ms_out) {
+  if (!tr || !ms_out) return set_error(NERF_E_INVALID, "null argument");
+  for (int i = 0; i < NERF_TRAIN_N_STAGES; ++i) ms_out[i] = 0.0f;
+  if (!tr->have_times) return NERF_OK;
+  DeviceGuardT dg(tr->device);
+  HIP_TRY(hipEventSynchronize(tr->ev[11]));
+  // event order: 0 | encode c | 1 | fwd c | 2 | render c | 3 | bwd c | 4 | reduce c | 5 |
+  //              encode f | 6 | fwd f | 7 | render f | 8 | bwd f | 9 | reduce f | 10 | update | 11
+  static const int stage_of[11] = {0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 4};
+  for (int i = 0; i < 11; ++i) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, tr->ev[i], tr->ev[i + 1]));
+    ms_out[stage_of[i]] += ms;
+  }
+  return NERF_OK;
+}
+
+}  // extern "C"

@@ -72,7 +72,33 @@ SIGNATURES = {
     "nerf_positional_encoding": (_c.c_int, [_c.c_int, _P, _c.c_long, _c.c_int, _P, _P]),
     "nerf_bf16x3_blob_bytes": (_c.c_size_t, []),
     "nerf_pack_weights_bf16x3": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P]),
+    "nerf_linspace01": (None, [_c.c_int, _FP]),
+    "nerf_trainer_create": (_c.c_int, [_c.c_int, _P, _c.POINTER(_FP), _c.POINTER(_FP), _c.c_int, _c.POINTER(_P)]),
+    "nerf_trainer_destroy": (None, [_P]),
+    "nerf_train_step": (_c.c_int, [_P, _P, _c.c_int, _c.c_int, _c.c_float, _FP, _P, _c.c_int, _P, _c.c_int, _P,
+                                   _P]),
+    "nerf_trainer_read": (_c.c_int, [_P, _c.c_int, _c.c_int, _c.POINTER(_FP), _c.c_int]),
+    "nerf_trainer_write_grads": (_c.c_int, [_P, _c.c_int, _c.POINTER(_FP), _c.c_int]),
+    "nerf_trainer_update": (_c.c_int, [_P, _P]),
+    "nerf_trainer_lr": (_c.c_double, [_P]),
+    "nerf_trainer_steps": (_c.c_long, [_P]),
+    "nerf_trainer_set_profiling": (_c.c_int, [_P, _c.c_int]),
+    "nerf_trainer_stage_ms": (_c.c_int, [_P, _FP]),
+    "nerf_trainer_gemm_flops": (_c.c_double, [_P]),
 }
+
+
+class TrainConfig(_c.Structure):
+    """nerf_train_config (include/nerf_mi355x.h)."""
+    _fields_ = [("lr", _c.c_double), ("beta1", _c.c_double), ("beta2", _c.c_double), ("eps", _c.c_double),
+                ("weight_decay", _c.c_double), ("lr_gamma", _c.c_double), ("grad_clip", _c.c_double),
+                ("n_coarse", _c.c_int), ("n_fine", _c.c_int), ("near_", _c.c_float), ("far_", _c.c_float)]
+
+
+NERF_TRAIN_NO_UPDATE = 1
+NERF_TR_PARAMS, NERF_TR_GRADS, NERF_TR_EXP_AVG, NERF_TR_EXP_AVG_SQ = 0, 1, 2, 3
+NERF_TRAIN_N_STAGES = 5
+TRAIN_STAGES = ("rays_encode", "forward_gemm", "render_heads", "backward_gemm", "reduce_update")
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -165,6 +191,13 @@ def f32_to_e4m3(x: np.ndarray) -> np.ndarray:
     out = np.zeros(a.size, np.uint8)
     lib.nerf_f32_to_e4m3(_fptr(a), a.size, out.ctypes.data_as(_P))
     return out.reshape(np.shape(x))
+
+
+def linspace01(n: int) -> np.ndarray:
+    """torch.linspace(0, 1, n) as the library computes it (host helper)."""
+    out = np.zeros(n, np.float32)
+    load_library().nerf_linspace01(n, _fptr(out))
+    return out
 
 
 def uniform_z(t_vals: np.ndarray, near: float, far: float) -> np.ndarray:

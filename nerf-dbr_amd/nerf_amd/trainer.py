@@ -1,0 +1,213 @@
+"""NeRFTrainer's training step on the MI355X.
+
+``MI355XTrainer`` mirrors the reference's ``NeRFTrainer``
+(``src/training/trainer.py:22-138``): the same configuration keys and defaults
+(``:25-81``), ``train_step(batch) -> float`` with the batch dict of the synthetic
+dataset (``src/data/loader.py:71-76``: image [H, W, 3], pose [4, 4], focal), the
+loss history lists and a reference-format checkpoint (``:376-384``).  The step
+itself is one call into the HIP library (``nerf_train_step``, include/nerf_mi355x.h):
+rays, stratified coarse and uniform fine samples, both networks forward and
+backward on the f32 MFMA, volume rendering with its backward, gradient clipping,
+Adam and the lr schedule all run on the device.  Nothing is computed in PyTorch;
+torch only provides device memory, the stream and the two random draws of a step
+(``torch.randperm`` for the rays, ``torch.rand`` for the stratification), which can
+also be injected for parity runs.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Mapping, Optional, Tuple
+
+import numpy as np
+
+from . import runtime as rt
+from .weights import LAYER_SPECS, StateDict, save_checkpoint, synthetic_state_dict, validate_state_dict
+
+# NeRFTrainer.__init__ defaults (trainer.py:50-75); main.py:25-61 overrides some of them
+DEFAULTS = {
+    "lr": 5e-4,
+    "weight_decay": 0.0,
+    "lr_decay": 0.1,
+    "decay_steps": 250000,
+    "n_coarse": 64,
+    "n_fine": 128,
+    "chunk_size": 1024,
+    "near": 2.0,
+    "far": 6.0,
+    "gradient_clipping": None,
+    "n_rays": 1024,
+    "checkpoint_frequency": 50,
+}
+
+
+def _shapes():
+    out = []
+    for name, o, i in LAYER_SPECS:
+        out.append((f"{name}.weight", (o, i)))
+        out.append((f"{name}.bias", (o,)))
+    return out
+
+
+class MI355XTrainer:
+    """NeRFTrainer on one MI355X: coarse + fine NeRFModel, one Adam over both, ExponentialLR."""
+
+    def __init__(self, config: Dict, coarse: Optional[Mapping[str, np.ndarray]] = None,
+                 fine: Optional[Mapping[str, np.ndarray]] = None, device_index: int = 0):
+        import torch
+
+        self.config = dict(DEFAULTS, **config)
+        c = self.config
+        if c.get("hidden_dim", 256) != 256 or c.get("position_encoding_levels", 10) != 10 or \
+                c.get("direction_encoding_levels", 4) != 4:
+            raise ValueError("the HIP kernels implement NeRFModel(pos_L=10, dir_L=4, hidden_dim=256)")
+        # fresh models when no state dicts are given: nn.Linear's init distribution
+        # (trainer.py:38-48 builds new NeRFModels)
+        coarse = coarse if coarse is not None else synthetic_state_dict(0, conditioned=False)
+        fine = fine if fine is not None else synthetic_state_dict(1, conditioned=False)
+        validate_state_dict(coarse)
+        validate_state_dict(fine)
+        self.device = f"cuda:{device_index}"
+        self.device_index = device_index
+        self.n_coarse, self.n_fine = int(c["n_coarse"]), int(c["n_fine"])
+        self.near, self.far = float(c["near"]), float(c["far"])
+        self.chunk_size = int(c["chunk_size"])
+        self.gradient_clipping = c["gradient_clipping"]
+        self.checkpoint_frequency = c["checkpoint_frequency"]
+        self.train_losses: list = []
+        self.val_losses: list = []
+        cfg = rt.TrainConfig()
+        cfg.lr = float(c["lr"])
+        cfg.beta1, cfg.beta2, cfg.eps = 0.9, 0.999, 1e-8
+        cfg.weight_decay = float(c["weight_decay"])
+        cfg.lr_gamma = float(c["lr_decay"]) ** (1 / c["decay_steps"])
+        cfg.grad_clip = float(self.gradient_clipping) if self.gradient_clipping is not None else 0.0
+        cfg.n_coarse, cfg.n_fine = self.n_coarse, self.n_fine
+        cfg.near_, cfg.far_ = self.near, self.far
+        self._cfg = cfg
+        self.lib = rt.load_library()
+        kc, pc = rt._param_list(coarse)
+        kf, pf = rt._param_list(fine)
+        h = ctypes.c_void_p()
+        rt._check(self.lib.nerf_trainer_create(device_index, ctypes.byref(cfg), pc, pf, rt.NERF_N_PARAMS,
+                                               ctypes.byref(h)))
+        del kc, kf
+        self._h = h
+        self._loss = torch.zeros(3, dtype=torch.float32, device=self.device)
+        self._gen = None
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.nerf_trainer_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ----------------------------------------------------------------- step --
+    def draws(self, height: int, width: int, n_rays: int, generator=None):
+        """The step's random draws as the reference makes them: torch.randperm over the
+        pixels, first n_rays (trainer.py:111), and U[0,1) per coarse sample (rendering.py:47)."""
+        import torch
+
+        sel = torch.randperm(height * width, device=self.device, generator=generator)[:n_rays]
+        t_rand = torch.rand(sel.numel(), self.n_coarse, device=self.device, generator=generator)
+        return sel.to(torch.int32), t_rand
+
+    def train_step(self, batch: Mapping, select_inds=None, t_rand=None, update: bool = True,
+                   sync: bool = True):
+        """NeRFTrainer.train_step (trainer.py:83-138): returns the step's loss (a float, as
+        loss.item(); with sync=False the device tensor [loss, mse_coarse, mse_fine])."""
+        import torch
+
+        image = batch["image"]
+        if not isinstance(image, torch.Tensor):
+            image = torch.as_tensor(np.asarray(image, dtype=np.float32))
+        image = image.to(self.device, torch.float32).contiguous()
+        if image.dim() != 3 or image.shape[-1] != 3:
+            raise ValueError(f"image must be [H, W, 3], got {tuple(image.shape)}")
+        height, width = int(image.shape[0]), int(image.shape[1])
+        pose = batch["pose"]
+        pose = pose.detach().cpu().numpy() if hasattr(pose, "detach") else np.asarray(pose)
+        pose = np.ascontiguousarray(pose.astype(np.float32).reshape(4, 4))
+        focal = float(batch["focal"])
+        n_rays = int(self.config["n_rays"])
+        if select_inds is None or t_rand is None:
+            s_draw, t_draw = self.draws(height, width, min(n_rays, height * width))
+            select_inds = s_draw if select_inds is None else select_inds
+            t_rand = t_draw if t_rand is None else t_rand
+        sel = torch.as_tensor(select_inds).to(self.device, torch.int32).contiguous()
+        tr = torch.as_tensor(t_rand).to(self.device, torch.float32).contiguous()
+        n = sel.numel()
+        if tuple(tr.shape) != (n, self.n_coarse):
+            raise ValueError(f"t_rand must be [{n}, {self.n_coarse}], got {tuple(tr.shape)}")
+        stream = torch.cuda.current_stream(self.device)
+        rt._check(self.lib.nerf_train_step(self._h, image.data_ptr(), height, width, focal, rt._fptr(pose),
+                                           sel.data_ptr(), n, tr.data_ptr(),
+                                           0 if update else rt.NERF_TRAIN_NO_UPDATE, self._loss.data_ptr(),
+                                           int(stream.cuda_stream)))
+        # keep the inputs alive until the queued step has consumed them
+        self._keep = (image, sel, tr)
+        if not sync:
+            return self._loss
+        return float(self._loss[0].item())
+
+    def update(self) -> None:
+        """Clip + Adam + schedule on the current gradients (the last part of train_step)."""
+        import torch
+
+        rt._check(self.lib.nerf_trainer_update(self._h, int(torch.cuda.current_stream(self.device).cuda_stream)))
+
+    # ---------------------------------------------------------------- state --
+    def _read(self, what: int, net: int) -> StateDict:
+        bufs = [np.zeros(shape, np.float32) for _, shape in _shapes()]
+        ptrs = (rt._FP * rt.NERF_N_PARAMS)(*[rt._fptr(b) for b in bufs])
+        rt._check(self.lib.nerf_trainer_read(self._h, what, net, ptrs, rt.NERF_N_PARAMS))
+        return {name: b for (name, _), b in zip(_shapes(), bufs)}
+
+    def state_dicts(self) -> Tuple[StateDict, StateDict]:
+        """(coarse, fine) parameters as NeRFModel state dicts (host arrays)."""
+        return self._read(rt.NERF_TR_PARAMS, 0), self._read(rt.NERF_TR_PARAMS, 1)
+
+    def grads(self, net: int) -> StateDict:
+        return self._read(rt.NERF_TR_GRADS, net)
+
+    def exp_avg(self, net: int) -> StateDict:
+        return self._read(rt.NERF_TR_EXP_AVG, net)
+
+    def exp_avg_sq(self, net: int) -> StateDict:
+        return self._read(rt.NERF_TR_EXP_AVG_SQ, net)
+
+    def write_grads(self, net: int, grads: Mapping[str, np.ndarray]) -> None:
+        keep, ptrs = rt._param_list(grads)
+        rt._check(self.lib.nerf_trainer_write_grads(self._h, net, ptrs, rt.NERF_N_PARAMS))
+        del keep
+
+    @property
+    def lr(self) -> float:
+        """optimizer.param_groups[0]['lr'] for the next step."""
+        return float(self.lib.nerf_trainer_lr(self._h))
+
+    @property
+    def steps(self) -> int:
+        return int(self.lib.nerf_trainer_steps(self._h))
+
+    def set_profiling(self, enable: bool) -> None:
+        rt._check(self.lib.nerf_trainer_set_profiling(self._h, 1 if enable else 0))
+
+    def stage_ms(self) -> Dict[str, float]:
+        ms = (ctypes.c_float * rt.NERF_TRAIN_N_STAGES)()
+        rt._check(self.lib.nerf_trainer_stage_ms(self._h, ms))
+        return dict(zip(rt.TRAIN_STAGES, list(ms)))
+
+    def gemm_flops(self) -> float:
+        """Algorithmic fp32 FLOP of the last step's GEMMs."""
+        return float(self.lib.nerf_trainer_gemm_flops(self._h))
+
+    def save_checkpoint(self, path: str) -> str:
+        """Reference-format checkpoint (trainer.py:376-384, model entries), loadable by
+        MI355XRenderer.setup."""
+        coarse, fine = self.state_dicts()
+        return save_checkpoint(path, coarse, fine)

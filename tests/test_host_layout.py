@@ -36,13 +36,20 @@ def test_library_exports_every_declared_symbol():
     lib = rt.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.nerf_abi_version() == 1
+    assert lib.nerf_abi_version() == 2
 
 
 def test_uniform_z_bit_exact(golden):
     g = golden("tvals")
     for s in [1, 2, 3, 16, 32, 64, 128, 192, 256]:
         assert np.array_equal(rt.uniform_z(g[f"t_{s}"], 2.0, 6.0), g[f"z_{s}"]), s
+
+
+def test_linspace01_matches_torch():
+    import torch
+
+    for n in list(range(1, 300)) + [511, 512, 513, 1000, 1023, 1024, 2048]:
+        assert np.array_equal(rt.linspace01(n), torch.linspace(0, 1, n).numpy()), n
 
 
 def test_pack_rejects_bad_input():
