@@ -108,7 +108,17 @@ constexpr long kGemmFloats = round_up(int(kBH + kHeadLd), 64);
 // Per-sample activation workspace (floats per sample; each array [P][ld])
 constexpr int kPeLd = 64, kDpeLd = 28;
 
-constexpr int BM = 128, BN = 128, BK = 16, LDT = 132;   // LDS row stride (floats)
+#ifndef NERF_TRAIN_BK
+#define NERF_TRAIN_BK 16
+#endif
+#ifndef NERF_TRAIN_SKCHUNK
+#define NERF_TRAIN_SKCHUNK 256   // samples per block of the skinny weight-gradient kernel
+#endif
+#ifndef NERF_TRAIN_PF
+#define NERF_TRAIN_PF 2   // k tiles staged ahead in registers (1 or 2)
+#endif
+constexpr int BM = 128, BN = 128, BK = NERF_TRAIN_BK, LDT = 132;   // LDS row stride (floats)
+constexpr int kLd = BK / 8;   // float4 loads per thread per operand and k tile (256 threads)
 
 // ------------------------------------------------------------------ GEMM --
 struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 % 4 == 0)
@@ -125,8 +135,9 @@ struct GemmArgs {
   float* c = nullptr;
   int ldc = 0;
   const float* bias = nullptr;      // kEpiBiasRelu: per column
-  const float* mask = nullptr;      // kEpiMask: C = acc where mask > 0, else 0
-  int ldm = 0;
+  const unsigned* mask = nullptr;   // kEpiMask: C = acc where the ReLU bit of (m, n) is set, else 0
+  unsigned* bits = nullptr;         // kEpiBiasRelu (optional): ReLU bits of C, [M][N / 32] words
+  int ldm = 0;                      // words per row of mask / bits
   float* bias_part = nullptr;       // kEpiPartial: [split][M] sums of A over the split's k
   int k_split = 0;                  // kEpiPartial: k range per blockIdx.z (multiple of BK)
   long c_split = 0;                 // kEpiPartial: floats per split partial
@@ -137,13 +148,13 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; 
 // One thread's two float4 of a BMxBK A tile (rows m0.., k0..).  Sources hold at
 // least round_up4(width) valid floats per row; elements past M/K are zero.
 template <bool kAK>
-__device__ __forceinline__ void load_a(const GemmArgs& g, int m0, int k0, int t, f32x4 (&ra)[2]) {
+__device__ __forceinline__ void load_a(const GemmArgs& g, int m0, int k0, int t, f32x4 (&ra)[kLd]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kLd; ++i) {
     const int idx = t + 256 * i;
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
     if (kAK) {
-      const int m = m0 + (idx >> 2), k = k0 + 4 * (idx & 3);
+      const int m = m0 + idx / (BK / 4), k = k0 + 4 * (idx % (BK / 4));
       if (m < g.M && k < g.K) {
         v = k < g.a.w1 ? ld4(g.a.p1 + long(m) * g.a.ld1 + k) : ld4(g.a.p2 + long(m) * g.a.ld2 + (k - g.a.w1));
 #pragma unroll
@@ -164,12 +175,12 @@ __device__ __forceinline__ void load_a(const GemmArgs& g, int m0, int k0, int t,
 }
 
 template <bool kAK>
-__device__ __forceinline__ void store_a(float* as, int t, const f32x4 (&ra)[2]) {
+__device__ __forceinline__ void store_a(float* as, int t, const f32x4 (&ra)[kLd]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kLd; ++i) {
     const int idx = t + 256 * i;
     if (kAK) {
-      const int m = idx >> 2, q = idx & 3;
+      const int m = idx / (BK / 4), q = idx % (BK / 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) as[(4 * q + j) * LDT + m] = ra[i][j];
     } else {
@@ -178,9 +189,9 @@ __device__ __forceinline__ void store_a(float* as, int t, const f32x4 (&ra)[2]) 
   }
 }
 
-__device__ __forceinline__ void load_b(const GemmArgs& g, int n0, int k0, int t, f32x4 (&rb)[2]) {
+__device__ __forceinline__ void load_b(const GemmArgs& g, int n0, int k0, int t, f32x4 (&rb)[kLd]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kLd; ++i) {
     const int idx = t + 256 * i;
     const int k = k0 + (idx >> 5), n = n0 + 4 * (idx & 31);
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -194,11 +205,32 @@ __device__ __forceinline__ void load_b(const GemmArgs& g, int n0, int k0, int t,
   }
 }
 
-__device__ __forceinline__ void store_b(float* bs, int t, const f32x4 (&rb)[2]) {
+__device__ __forceinline__ void store_b(float* bs, int t, const f32x4 (&rb)[kLd]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kLd; ++i) {
     const int idx = t + 256 * i;
     *(f32x4*)(bs + (idx >> 5) * LDT + 4 * (idx & 31)) = rb[i];
+  }
+}
+
+// One LDS k tile into the wave's 64x64 accumulator block (2x2 MFMA tiles); with
+// kEpiPartial the first column tile also sums A over k for row t (the bias gradient).
+template <int kEpi>
+__device__ __forceinline__ void gemm_tile(const float* __restrict__ as, const float* __restrict__ bs,
+                                          f32x16 (&acc)[2][2], float& bsum, int wm, int wn, int h, int l32, int t) {
+#pragma unroll
+  for (int kk = 0; kk < BK / 2; ++kk) {
+    const int k = 2 * kk + h;
+    const float a0 = as[k * LDT + wm * 64 + l32], a1 = as[k * LDT + wm * 64 + 32 + l32];
+    const float b0 = bs[k * LDT + wn * 64 + l32], b1 = bs[k * LDT + wn * 64 + 32 + l32];
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+  }
+  if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM) {
+#pragma unroll
+    for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, as[kr * LDT + t]);
   }
 }
 
@@ -224,59 +256,80 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   float bsum = 0.0f;
-  f32x4 ra[2], rb[2];
+  auto load_tile = [&](int it, f32x4 (&ra)[kLd], f32x4 (&rb)[kLd]) {
+    load_a<kAK>(g, m0, kbeg + it * BK, t, ra);
+    load_b(g, n0, kbeg + it * BK, t, rb);
+  };
+  auto store_tile = [&](int buf, const f32x4 (&ra)[kLd], const f32x4 (&rb)[kLd]) {
+    store_a<kAK>(As[buf], t, ra);
+    store_b(Bs[buf], t, rb);
+  };
+#if NERF_TRAIN_PF == 1
+  f32x4 ra[kLd], rb[kLd];
   if (nt > 0) {
-    load_a<kAK>(g, m0, kbeg, t, ra);
-    load_b(g, n0, kbeg, t, rb);
-    store_a<kAK>(As[0], t, ra);
-    store_b(Bs[0], t, rb);
+    load_tile(0, ra, rb);
+    store_tile(0, ra, rb);
     __syncthreads();
   }
   for (int it = 0; it < nt; ++it) {
     const int cur = it & 1;
     const bool more = it + 1 < nt;
-    if (more) {
-      load_a<kAK>(g, m0, kbeg + (it + 1) * BK, t, ra);
-      load_b(g, n0, kbeg + (it + 1) * BK, t, rb);
-    }
-    const float* as = As[cur];
-    const float* bs = Bs[cur];
-#pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      const int k = 2 * kk + h;
-      const float a0 = as[k * LDT + wm * 64 + l32], a1 = as[k * LDT + wm * 64 + 32 + l32];
-      const float b0 = bs[k * LDT + wn * 64 + l32], b1 = bs[k * LDT + wn * 64 + 32 + l32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM) {
-#pragma unroll
-      for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, as[kr * LDT + t]);
-    }
-    if (more) {
-      store_a<kAK>(As[cur ^ 1], t, ra);
-      store_b(Bs[cur ^ 1], t, rb);
-    }
+    if (more) load_tile(it + 1, ra, rb);
+    gemm_tile<kEpi>(As[cur], Bs[cur], acc, bsum, wm, wn, h, l32, t);
+    if (more) store_tile(cur ^ 1, ra, rb);
     __syncthreads();
   }
+#else
+  // k tiles staged two ahead: registers hold tile it+1 (landing) and tile it+2 (issued
+  // this iteration) while LDS buffer it&1 is consumed; the register sets alternate by
+  // iteration parity, so the loop is unrolled by two
+  f32x4 ra0[kLd], rb0[kLd], ra1[kLd], rb1[kLd];
+  if (nt > 0) {
+    load_tile(0, ra0, rb0);
+    store_tile(0, ra0, rb0);
+    if (nt > 1) load_tile(1, ra1, rb1);
+    __syncthreads();
+  }
+  int it = 0;
+  for (; it + 1 < nt; it += 2) {
+    if (it + 2 < nt) load_tile(it + 2, ra0, rb0);
+    gemm_tile<kEpi>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);
+    store_tile(1, ra1, rb1);
+    __syncthreads();
+    if (it + 3 < nt) load_tile(it + 3, ra1, rb1);
+    gemm_tile<kEpi>(As[1], Bs[1], acc, bsum, wm, wn, h, l32, t);
+    if (it + 2 < nt) store_tile(0, ra0, rb0);
+    __syncthreads();
+  }
+  if (it < nt) gemm_tile<kEpi>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);   // odd tile count: the last
+#endif
   float* c = g.c + (kEpi == kEpiPartial ? long(blockIdx.z) * g.c_split : 0L);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + wn * 64 + j * 32 + l32;
-      if (n >= g.N) continue;
-      const float bn = kEpi == kEpiBiasRelu ? g.bias[n] : 0.0f;
+      const bool nok = n < g.N;
+      const int word = (n0 + wn * 64 + j * 32) >> 5;   // this 32-column group's word in a row
+      const float bn = kEpi == kEpiBiasRelu && nok ? g.bias[n] : 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
-        if (m >= g.M) continue;
+        const bool ok = nok && m < g.M;
         float v = acc[i][j][r];
-        if (kEpi == kEpiBiasRelu) v = relu(__fadd_rn(v, bn));
-        if (kEpi == kEpiMask) v = g.mask[long(m) * g.ldm + n] > 0.0f ? v : 0.0f;
-        c[long(m) * g.ldc + n] = v;
+        if (kEpi == kEpiBiasRelu) {
+          v = relu(__fadd_rn(v, bn));
+          if (g.bits) {
+            // ReLU bits for the backward pass (1 bit instead of the 4-B activation):
+            // lanes 0-31 are row acc_row(r, 0), lanes 32-63 row acc_row(r, 1)
+            const unsigned long long bal = __ballot(ok && v > 0.0f);
+            if (l32 == 0 && m < g.M) g.bits[long(m) * g.ldm + word] = unsigned(h ? bal >> 32 : bal);
+          }
+        }
+#ifndef NERF_TRAIN_ABLATE_MASK
+        if (kEpi == kEpiMask && ok) v = (g.mask[long(m) * g.ldm + word] >> l32) & 1u ? v : 0.0f;
+#endif
+        if (ok) c[long(m) * g.ldc + n] = v;
       }
     }
   if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM && m0 + t < g.M)
@@ -490,18 +543,76 @@ __global__ void reduce_grads_kernel(RedJobs jobs, float* __restrict__ grads) {
   const RedJob& jb = jobs.j[blockIdx.y];
   const long e = long(blockIdx.x) * blockDim.x + threadIdx.x;
   const long mn = long(jb.M) * jb.N;
+  const float* src;
+  long stride, dst;
   if (e < mn) {
     const int m = int(e / jb.N), n = int(e - long(m) * jb.N);
     const bool g0 = m < jb.r1;
     if (n >= (g0 ? jb.nw0 : jb.nw1)) return;
-    float s = 0.0f;
-    for (int k = 0; k < jb.splits; ++k) s = __fadd_rn(s, jb.part[k * mn + e]);
-    grads[g0 ? jb.w0 + long(m) * jb.ld0 + n : jb.w1 + long(m - jb.r1) * jb.ld1 + n] = s;
+    src = jb.part + e;
+    stride = mn;
+    dst = g0 ? jb.w0 + long(m) * jb.ld0 + n : jb.w1 + long(m - jb.r1) * jb.ld1 + n;
   } else if (e < mn + jb.M) {
     const int m = int(e - mn);
-    float s = 0.0f;
-    for (int k = 0; k < jb.splits; ++k) s = __fadd_rn(s, jb.bpart[long(k) * jb.M + m]);
-    grads[m < jb.r1 ? jb.b0 + m : jb.b1 + (m - jb.r1)] = s;
+    src = jb.bpart + m;
+    stride = jb.M;
+    dst = m < jb.r1 ? jb.b0 + m : jb.b1 + (m - jb.r1);
+  } else {
+    return;
+  }
+  // four interleaved partial sums (split k into sum k % 4), then combined: a fixed
+  // order, so the result is deterministic, with four loads in flight per thread
+  float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  int k = 0;
+  for (; k + 4 <= jb.splits; k += 4)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s4[q] = __fadd_rn(s4[q], src[(k + q) * stride]);
+  for (; k < jb.splits; ++k) s4[k & 3] = __fadd_rn(s4[k & 3], src[k * stride]);
+  grads[dst] = __fadd_rn(__fadd_rn(s4[0], s4[1]), __fadd_rn(s4[2], s4[3]));
+}
+
+// Weight gradients of the skinny layers (colour-1: 3 rows over the 128 colour-0 outputs;
+// density: 1 row over the 256 trunk outputs): partial[split][m][n] = sum over the
+// split's samples of A[p][m] * B[p][n], and the bias partials sum_p A[p][m].
+// 1024 threads: column n = t % 256, sample phase t / 256 (every 4th sample of the
+// split); the four phase sums are then added in a fixed order.  B rows are read whole.
+__global__ __launch_bounds__(1024) void skinny_wgrad_kernel(const float* __restrict__ A, int lda, int M,
+                                                            const float* __restrict__ B, int ldb, int N, long P,
+                                                            int chunk, float* __restrict__ part,
+                                                            float* __restrict__ bpart) {
+  __shared__ float red[4][4][256];
+  __shared__ float bred[4][4];
+  const int split = blockIdx.x, n = threadIdx.x & 255, ph = threadIdx.x >> 8;
+  const long p0 = long(split) * chunk;
+  const long p1 = p0 + chunk < P ? p0 + chunk : P;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 4
+  for (long p = p0 + ph; p < p1; p += 4) {
+    const float b = n < N ? B[p * ldb + n] : 0.0f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (m < M) {
+        const float a = A[p * lda + m];
+        acc[m] = fmaf(a, b, acc[m]);
+        bs[m] = __fadd_rn(bs[m], a);
+      }
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) red[ph][m][n] = acc[m];
+  if (n == 0)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) bred[ph][m] = bs[m];
+  __syncthreads();
+  if (ph == 0) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (m < M) {
+        if (n < N)
+          part[(long(split) * M + m) * N + n] =
+              __fadd_rn(__fadd_rn(red[0][m][n], red[1][m][n]), __fadd_rn(red[2][m][n], red[3][m][n]));
+        if (n == 0)
+          bpart[long(split) * M + m] = __fadd_rn(__fadd_rn(bred[0][m], bred[1][m]), __fadd_rn(bred[2][m], bred[3][m]));
+      }
   }
 }
 
@@ -683,12 +794,13 @@ inline size_t al64(size_t x) { return (x + 63) / 64 * 64; }
 // Per-net activation arrays inside the workspace.
 struct Acts {
   float *pe, *dpe, *h[8], *hc, *rgbs, *dpre, *tb, *dhc, *d0, *d1;
+  unsigned* mb[8];   // ReLU bits of h[l]: [P][8] words
 };
 
 size_t acts_floats(long P) {
   const size_t p = size_t(P);
   return al64(p * kPeLd) + al64(p * kDpeLd) + 8 * al64(p * kH) + al64(p * kHeadLd) + 2 * al64(p * 4) + al64(p) +
-         al64(p * kHeadLd) + 2 * al64(p * kH);
+         al64(p * kHeadLd) + 2 * al64(p * kH) + 8 * al64(p * (kH / 32));
 }
 
 size_t head_floats(int n_rays, int n_coarse) {
@@ -714,6 +826,7 @@ Acts carve_acts(float* base, long P) {
   a.dhc = take(p * kHeadLd);
   a.d0 = take(p * kH);
   a.d1 = take(p * kH);
+  for (auto& b : a.mb) b = (unsigned*)take(p * (kH / 32));
   return a;
 }
 
@@ -782,6 +895,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     g.b = Src2{gw + wt_off(l), nullptr, kH, 0, 0x7fffffff};
     g.c = a.h[l], g.ldc = kH;
     g.bias = prm + b_off(l);
+    g.bits = a.mb[l], g.ldm = kH / 32;
     HIP_TRY((gemm<true, kEpiBiasRelu>(g, 1, s)));
   }
   {
@@ -809,8 +923,16 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
 
   // backward GEMMs; weight gradients as split partials
   size_t cur = 0;
-  WJob jc1 = plan_wjob(3, kC0, P, cur);
-  WJob jh = plan_wjob(kHeadN, kHeadK, P, cur);
+  constexpr int kSkinnyChunk = NERF_TRAIN_SKCHUNK;
+  const int sk_splits = int(blocks_for(P, kSkinnyChunk));
+  WJob jc1{3, kC0, sk_splits, kSkinnyChunk, 0, 0}, jd{1, kH, sk_splits, kSkinnyChunk, 0, 0};
+  for (WJob* j : {&jc1, &jd}) {
+    j->off = cur;
+    cur += al64(size_t(j->splits) * j->M * j->N);
+    j->boff = cur;
+    cur += al64(size_t(j->splits) * j->M);
+  }
+  WJob jh = plan_wjob(kC0, kHeadK, P, cur);
   WJob jl[8];
   for (int l = 7; l >= 0; --l) jl[l] = plan_wjob(kH, kTrunkIn[l], P, cur);
   if ((rc = grow_buf(tr->part, tr->part_cap, cur, "gradient partials")) != NERF_OK) return rc;
@@ -825,7 +947,12 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     g.c_split = long(j.M) * j.N;
     return gemm<false, kEpiPartial>(g, j.splits, s);
   };
-  HIP_TRY(wgrad(jc1, a.dpre, 4, Src2{a.hc, nullptr, kHeadLd, 0, 0x7fffffff}));
+  hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jc1.splits), dim3(1024), 0, s, (const float*)a.dpre, 4, 3,
+                     (const float*)a.hc, kHeadLd, kC0, P, kSkinnyChunk, tr->part + jc1.off, tr->part + jc1.boff);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jd.splits), dim3(1024), 0, s, (const float*)a.dpre + 3, 4, 1,
+                     (const float*)a.h[7], kH, kH, P, kSkinnyChunk, tr->part + jd.off, tr->part + jd.boff);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(wgrad(jh, a.dhc, kHeadLd, Src2{a.h[7], a.dpe, kH, kDpeLd, kH}));
   {
     GemmArgs g;   // d h7 = dhc . [colour-0 rows; density row] over the hidden inputs, ReLU mask of h7
@@ -833,7 +960,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     g.a = Src2{a.dhc, nullptr, kHeadLd, 0, 0x7fffffff};
     g.b = Src2{gw + kWcH, nullptr, kH, 0, 0x7fffffff};
     g.c = a.d0, g.ldc = kH;
-    g.mask = a.h[7], g.ldm = kH;
+    g.mask = a.mb[7], g.ldm = kH / 32;
     HIP_TRY((gemm<true, kEpiMask>(g, 1, s)));
   }
   float* dz = a.d0;
@@ -850,7 +977,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     g.a = Src2{dz, nullptr, kH, 0, 0x7fffffff};
     g.b = l == 4 ? Src2{gw + kW4h, nullptr, kH, 0, 0x7fffffff} : Src2{prm + w_off(l), nullptr, kH, 0, 0x7fffffff};
     g.c = dn, g.ldc = kH;
-    g.mask = a.h[l - 1], g.ldm = kH;
+    g.mask = a.mb[l - 1], g.ldm = kH / 32;
     HIP_TRY((gemm<true, kEpiMask>(g, 1, s)));
     std::swap(dz, dn);
   }
@@ -867,10 +994,11 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     job(l, jl[l], kH, w_off(l), b_off(l), kTrunkIn[l], kTrunkIn[l], 0, 0, 0, 0);
     maxe = std::max(maxe, long(jl[l].M) * jl[l].N + jl[l].M);
   }
-  job(8, jh, kC0, kFC0W, kFC0B, kHeadK, kHeadK, kFDensW, kFDensB, kH, kH);
-  job(9, jc1, 3, kFC1W, kFC1B, kC0, kC0, 0, 0, 0, 0);
+  job(8, jh, kC0, kFC0W, kFC0B, kHeadK, kHeadK, 0, 0, 0, 0);
+  job(9, jd, 1, kFDensW, kFDensB, kH, kH, 0, 0, 0, 0);
+  job(10, jc1, 3, kFC1W, kFC1B, kC0, kC0, 0, 0, 0, 0);
   maxe = std::max(maxe, long(jh.M) * jh.N + jh.M);
-  hipLaunchKernelGGL(reduce_grads_kernel, dim3(blocks_for(maxe, 256), 10), dim3(256), 0, s, jobs, grads);
+  hipLaunchKernelGGL(reduce_grads_kernel, dim3(blocks_for(maxe, 256), 11), dim3(256), 0, s, jobs, grads);
   HIP_TRY(hipGetLastError());
   tr->gemm_flops += 2.0 * gemm_macs_per_sample() * double(P);
   return NERF_OK;
