@@ -214,15 +214,19 @@ def sharded_hierarchical(ckpt, pose, local, rank, world, width, height, n_warm=2
 TRAIN_RAYS = 2048            # main.py:40 (get_default_config n_rays)
 
 
-def training_leg(local, n_steps, cpu_seconds):
-    """NeRFTrainer.train_step on this GPU with main.py's configuration
+def training_leg(local, rank, world, n_steps, cpu_seconds):
+    """NeRFTrainer.train_step on the GPU(s) with main.py's configuration
     (2048 rays, 64 stratified coarse + 128 uniform fine samples, Adam lr 3e-4, weight
     decay 1e-6, clip 1.0): steps/s and rays/s with the step's own draws (torch.randperm,
     torch.rand on the device) inside the timed region, the GEMMs' fp32 MFMA rate from
-    the trainer's HIP events, and the oracle's step timed on the host cores."""
+    the trainer's HIP events, and the oracle's step timed on the host cores.  At N > 1
+    the step is data parallel (nerf_amd.distributed.train_step_sharded): each rank takes
+    2048/N of the step's rays and one RCCL all-reduce sums the gradients (strong scaling:
+    the step is fixed)."""
     import numpy as np
     import torch
 
+    from nerf_amd import distributed as D
     from nerf_amd import weights as W
     from nerf_amd.trainer import MI355XTrainer
     from oracle import nerf_train_oracle as T
@@ -237,31 +241,43 @@ def training_leg(local, n_steps, cpu_seconds):
     pose[2, 3] = 4.0
     batch = {"image": image, "pose": pose, "focal": 0.5 * w / np.tan(0.5 * 0.6911112070083618)}
     tr.set_profiling(True)
-    losses = [tr.train_step(batch) for _ in range(2)]
-    torch.cuda.synchronize()
+    gen = torch.Generator(device=f"cuda:{local}")
+
+    def step(i):
+        if world == 1:
+            return tr.train_step(batch, sync=False)
+        gen.manual_seed(1000 + i)            # the same step draw on every rank
+        sel, t_rand = tr.draws(h, w, TRAIN_RAYS, generator=gen)
+        return D.train_step_sharded(tr, batch, sel, t_rand)
+
+    losses = [float(step(i)[0].item()) for i in range(2)]
+    sync_barrier(world)
     t0 = time.perf_counter()
     stages = []
-    for _ in range(n_steps):
-        tr.train_step(batch, sync=False)
+    for i in range(n_steps):
+        step(2 + i)
         stages.append(tr.stage_ms())
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / n_steps
-    losses.append(tr.train_step(batch))
+    sync_barrier(world)
+    dt = D.reduce_max(time.perf_counter() - t0) / n_steps
+    losses.append(float(step(2 + n_steps)[0].item()))
     st = {k: float(np.mean([s[k] for s in stages])) for k in stages[0]}
     gemm_ms = st["forward_gemm"] + st["backward_gemm"]
     flop = tr.gemm_flops()
     out = {"workload": "NeRFTrainer.train_step, main.py config: 2048 rays of a 400x400 target, 64 stratified "
                        "coarse + 128 uniform fine samples, both nets forward+backward, clip 1.0, Adam, ExponentialLR",
-           "dtype": "fp32", "steps": n_steps, "ms_per_step": 1e3 * dt, "steps_per_s": 1.0 / dt,
-           "rays_per_s": TRAIN_RAYS / dt, "stage_ms": st,
-           "gemm": {"flop_per_step": flop, "ms_per_step": gemm_ms, "achieved": flop / (gemm_ms * 1e-3) / 1e12,
+           "dtype": "fp32", "steps": n_steps, "n_gpus": world, "ms_per_step": 1e3 * dt, "steps_per_s": 1.0 / dt,
+           "rays_per_s": TRAIN_RAYS / dt, "stage_ms_rank0": st,
+           "parallelism": "1 GPU" if world == 1 else f"data parallel x{world}: 2048/{world} rays per rank + "
+                                                     f"{'RCCL' if torch.distributed.get_backend() == 'nccl' else 'gloo'} "
+                                                     f"all-reduce of the gradients (4.2 MB)",
+           "gemm": {"flop_per_step_rank0": flop, "ms_per_step": gemm_ms, "achieved": flop / (gemm_ms * 1e-3) / 1e12,
                     "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
                     "frac": flop / (gemm_ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"],
                     "note": "all forward, backward-data and weight-gradient GEMMs of both nets (unpadded "
                             "MACs x 2) over the forward_gemm + backward_gemm stages (HIP events)"},
            "loss_first_last": [losses[0], losses[-1]]}
     tr.close()
-    if cpu_seconds > 0:
+    if cpu_seconds > 0 and rank == 0 and world == 1:
         # the oracle's step (PyTorch-CPU autograd restatement of NeRFTrainer.train_step)
         import math
 
@@ -481,8 +497,8 @@ def main():
                 rs[p].hip.set_profiling(True)
         extra["readme_grid"] = readme_grid(rs, pose, rank, world)
 
-    if world == 1 and not args.no_train:
-        extra["training"] = training_leg(local, args.train_steps, min(10.0, args.cpu_seconds / 3))
+    if not args.no_train and not (world > 1 and args.no_extras):
+        extra["training"] = training_leg(local, rank, world, args.train_steps, min(10.0, args.cpu_seconds / 3))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

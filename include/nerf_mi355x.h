@@ -260,6 +260,23 @@ int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width,
                     const float* c2w, const int32_t* select, int n_rays, const float* t_rand, int flags,
                     float* loss_out, void* stream);
 
+/* Data-parallel training (one process per GPU): the gradients of this rank's share
+ * of a step's rays (select / t_rand rows of the share), with the MSE normalised by the whole
+ * step's ray count (the mean over n_rays_total x 3, trainer.py:117-119), so that the sum over
+ * ranks -- one all-reduce of the gradient store -- is the full step's gradient.  No update:
+ * every rank then runs nerf_trainer_update on the reduced gradients and the replicas stay
+ * identical.  loss_out (device [3], may be NULL): this share's part of each mean. */
+int nerf_train_backward(nerf_trainer* tr, const float* image, int height, int width, float focal,
+                        const float* c2w, const int32_t* select, int n_rays, int n_rays_total,
+                        const float* t_rand, float* loss_out, void* stream);
+/* Floats per net in the flat gradient / parameter order (state-dict order, 530,052). */
+#define NERF_TRAIN_NET_FLOATS 530052
+/* Makes a caller-owned device buffer of 2 * NERF_TRAIN_NET_FLOATS floats (coarse, then fine; each
+ * net's 22 tensors in state-dict order, row-major) the trainer's gradient store -- e.g. a tensor
+ * that torch.distributed all-reduces between nerf_train_backward and nerf_trainer_update.  The
+ * current gradients are copied in; NULL returns to the trainer's own store. */
+int nerf_trainer_set_grad_buffer(nerf_trainer* tr, float* grads_dev);
+
 /* Reads one net's state into 22 host buffers (state-dict order and shapes; synchronous):
  * what = NERF_TR_PARAMS, NERF_TR_GRADS (the last step's gradients, clipped when that step
  * updated), NERF_TR_EXP_AVG or NERF_TR_EXP_AVG_SQ (Adam's moment estimates). */

@@ -636,8 +636,9 @@ __global__ void sumsq_kernel(const float* __restrict__ g, long n, double* __rest
 // Loss (trainer.py:117-119: mean over [n_rays][3] per net, summed) and the clip
 // coefficient of clip_grad_norm_: min(max_norm / (total_norm + 1e-6), 1).
 // out: [0] loss, [1] coarse MSE, [2] fine MSE; coef: the factor Adam applies.
-__global__ void finalize_kernel(const float* __restrict__ loss_ray, int n_rays, const double* __restrict__ sq_part,
-                                int n_part, float max_norm, float* __restrict__ out, float* __restrict__ coef) {
+__global__ void finalize_kernel(const float* __restrict__ loss_ray, int n_rays, int n_total,
+                                const double* __restrict__ sq_part, int n_part, float max_norm, float* __restrict__ out,
+                                float* __restrict__ coef) {
   __shared__ double red[3][256];
   double a = 0.0, b = 0.0, q = 0.0;
   for (int i = threadIdx.x; i < n_rays; i += blockDim.x) {
@@ -656,7 +657,7 @@ __global__ void finalize_kernel(const float* __restrict__ loss_ray, int n_rays, 
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float denom = float(3.0 * n_rays);
+    const float denom = float(3.0 * n_total);
     const float mc = __fdiv_rn(float(red[0][0]), denom), mf = __fdiv_rn(float(red[1][0]), denom);
     if (out) {
       out[0] = __fadd_rn(mc, mf);
@@ -745,7 +746,8 @@ struct nerf_trainer {
   double lr = 0.0;
   long steps = 0;
   float* params = nullptr;   // [2][kNetFloats]
-  float* grads = nullptr;
+  float* grads = nullptr;    // the gradient store in use: own_grads or a caller's buffer
+  float* own_grads = nullptr;
   float* m = nullptr;
   float* v = nullptr;
   float* gemmw = nullptr;    // [2][kGemmFloats]
@@ -869,7 +871,7 @@ double gemm_macs_per_sample() {
 
 // Forward + backward of one net on P = n_rays * S samples; gradients into grads (flat).
 int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d, const float* target,
-             const float* z, int z_stride, int n_rays, int S, float* loss_ray, hipStream_t s, int ev0) {
+             const float* z, int z_stride, int n_rays, int n_total, int S, float* loss_ray, hipStream_t s, int ev0) {
   const long P = long(n_rays) * S;
   Acts a = carve_acts(tr->ws + head_floats(n_rays, tr->cfg.n_coarse), P);
   const float* prm = tr->params + net * kNetFloats;
@@ -912,7 +914,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   // colour head, volume render + loss, their backward (rendering.py:102-143, trainer.py:117-126)
   hipLaunchKernelGGL(color_out_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, a.hc, prm, P, (f32x4*)a.rgbs);
   HIP_TRY(hipGetLastError());
-  const float gnorm = float(2.0 / (3.0 * n_rays));
+  const float gnorm = float(2.0 / (3.0 * n_total));   // mse_loss backward over the whole step's rays
   hipLaunchKernelGGL(render_train_kernel, dim3(blocks_for(n_rays, 64)), dim3(64), 0, s, (const f32x4*)a.rgbs, z,
                      z_stride, rays_d, target, n_rays, S, gnorm, a.tb, (f32x4*)a.dpre, loss_ray);
   HIP_TRY(hipGetLastError());
@@ -1012,7 +1014,7 @@ int update_impl(nerf_trainer* tr, hipStream_t s) {
     hipLaunchKernelGGL(sumsq_kernel, dim3(kSqBlocks), dim3(256), 0, s, tr->grads, n, sq);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)nullptr, 0,
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)nullptr, 0, 1,
                      clip ? (const double*)sq : (const double*)nullptr, kSqBlocks, float(tr->cfg.grad_clip),
                      (float*)nullptr, tr->scal);
   HIP_TRY(hipGetLastError());
@@ -1077,8 +1079,9 @@ int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* c
     return rc;
   };
   const size_t bytes = sizeof(float) * 2 * kNetFloats;
-  for (float** p : {&tr->params, &tr->grads, &tr->m, &tr->v})
+  for (float** p : {&tr->params, &tr->own_grads, &tr->m, &tr->v})
     if (hipMalloc((void**)p, bytes) != hipSuccess) return fail(set_error(NERF_E_HIP, "hipMalloc trainer state"));
+  tr->grads = tr->own_grads;
   if (hipMalloc((void**)&tr->gemmw, sizeof(float) * 2 * kGemmFloats) != hipSuccess ||
       hipMalloc((void**)&tr->ztab, sizeof(float) * 2048) != hipSuccess ||
       hipMalloc((void**)&tr->scal, sizeof(float) * (4 + 2 * kSqBlocks)) != hipSuccess ||
@@ -1120,7 +1123,7 @@ void nerf_trainer_destroy(nerf_trainer* tr) {
   if (!tr) return;
   DeviceGuardT dg(tr->device);
   (void)hipDeviceSynchronize();
-  for (float* p : {tr->params, tr->grads, tr->m, tr->v, tr->gemmw, tr->ztab, tr->scal, tr->ws, tr->part})
+  for (float* p : {tr->params, tr->own_grads, tr->m, tr->v, tr->gemmw, tr->ztab, tr->scal, tr->ws, tr->part})
     if (p) (void)hipFree(p);
   if (tr->bad) (void)hipFree(tr->bad);
   for (auto& e : tr->ev)
@@ -1128,9 +1131,15 @@ void nerf_trainer_destroy(nerf_trainer* tr) {
   delete tr;
 }
 
-int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width, float focal, const float* c2w,
-                    const int32_t* select, int n_rays, const float* t_rand, int flags, float* loss_out, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int train_impl(nerf_trainer* tr, const float* image, int height, int width, float focal, const float* c2w,
+               const int32_t* select, int n_rays, int n_total, const float* t_rand, bool update, float* loss_out,
+               void* stream) {
   if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  if (n_total < n_rays) return set_error(NERF_E_INVALID, "nerf_train: n_rays_total %d < n_rays %d", n_total, n_rays);
   if (!image || !c2w || !select || !t_rand) return set_error(NERF_E_INVALID, "nerf_train_step: null argument");
   if (height <= 0 || width <= 0 || n_rays <= 0 || long(height) * width > 0x7fffffffL)
     return set_error(NERF_E_INVALID, "nerf_train_step: bad sizes %dx%d, %d rays", height, width, n_rays);
@@ -1168,20 +1177,48 @@ int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width,
   HIP_TRY(hipGetLastError());
   // coarse samples stratified with the injected draw (rendering.py:42-47)
   HIP_TRY(launch_sample(tr->ztab, t_rand, n_rays, tr->cfg.n_coarse, nullptr, nullptr, zc, nullptr, s));
-  if ((rc = net_pass(tr, 0, rays_o, rays_d, target, zc, tr->cfg.n_coarse, n_rays, tr->cfg.n_coarse, loss_ray, s, 0)) !=
-      NERF_OK)
+  if ((rc = net_pass(tr, 0, rays_o, rays_d, target, zc, tr->cfg.n_coarse, n_rays, n_total, tr->cfg.n_coarse, loss_ray,
+                     s, 0)) != NERF_OK)
     return rc;
   if ((rc = mark(5)) != NERF_OK) return rc;
-  if ((rc = net_pass(tr, 1, rays_o, rays_d, target, tr->ztab + 1024, 0, n_rays, tr->cfg.n_fine, loss_ray + n_rays, s,
-                     5)) != NERF_OK)
+  if ((rc = net_pass(tr, 1, rays_o, rays_d, target, tr->ztab + 1024, 0, n_rays, n_total, tr->cfg.n_fine,
+                     loss_ray + n_rays, s, 5)) != NERF_OK)
     return rc;
   if ((rc = mark(10)) != NERF_OK) return rc;
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)loss_ray, n_rays, (const double*)nullptr,
-                     0, 0.0f, loss_out, (float*)nullptr);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)loss_ray, n_rays, n_total,
+                     (const double*)nullptr, 0, 0.0f, loss_out, (float*)nullptr);
   HIP_TRY(hipGetLastError());
-  if (!(flags & NERF_TRAIN_NO_UPDATE) && (rc = update_impl(tr, s)) != NERF_OK) return rc;
+  if (update && (rc = update_impl(tr, s)) != NERF_OK) return rc;
   if ((rc = mark(11)) != NERF_OK) return rc;
   tr->have_times = tr->profiling;
+  return NERF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width, float focal, const float* c2w,
+                    const int32_t* select, int n_rays, const float* t_rand, int flags, float* loss_out, void* stream) {
+  return train_impl(tr, image, height, width, focal, c2w, select, n_rays, n_rays, t_rand,
+                    !(flags & NERF_TRAIN_NO_UPDATE), loss_out, stream);
+}
+
+int nerf_train_backward(nerf_trainer* tr, const float* image, int height, int width, float focal, const float* c2w,
+                        const int32_t* select, int n_rays, int n_rays_total, const float* t_rand, float* loss_out,
+                        void* stream) {
+  return train_impl(tr, image, height, width, focal, c2w, select, n_rays, n_rays_total, t_rand, false, loss_out,
+                    stream);
+}
+
+int nerf_trainer_set_grad_buffer(nerf_trainer* tr, float* grads_dev) {
+  if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  float* next = grads_dev ? grads_dev : tr->own_grads;
+  if (next == tr->grads) return NERF_OK;
+  DeviceGuardT dg(tr->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(next, tr->grads, sizeof(float) * 2 * kNetFloats, hipMemcpyDeviceToDevice));
+  tr->grads = next;
   return NERF_OK;
 }
 

@@ -77,6 +77,9 @@ SIGNATURES = {
     "nerf_trainer_destroy": (None, [_P]),
     "nerf_train_step": (_c.c_int, [_P, _P, _c.c_int, _c.c_int, _c.c_float, _FP, _P, _c.c_int, _P, _c.c_int, _P,
                                    _P]),
+    "nerf_train_backward": (_c.c_int, [_P, _P, _c.c_int, _c.c_int, _c.c_float, _FP, _P, _c.c_int, _c.c_int, _P,
+                                       _P, _P]),
+    "nerf_trainer_set_grad_buffer": (_c.c_int, [_P, _P]),
     "nerf_trainer_read": (_c.c_int, [_P, _c.c_int, _c.c_int, _c.POINTER(_FP), _c.c_int]),
     "nerf_trainer_write_grads": (_c.c_int, [_P, _c.c_int, _c.POINTER(_FP), _c.c_int]),
     "nerf_trainer_update": (_c.c_int, [_P, _P]),
@@ -96,6 +99,7 @@ class TrainConfig(_c.Structure):
 
 
 NERF_TRAIN_NO_UPDATE = 1
+NERF_TRAIN_NET_FLOATS = 530052
 NERF_TR_PARAMS, NERF_TR_GRADS, NERF_TR_EXP_AVG, NERF_TR_EXP_AVG_SQ = 0, 1, 2, 3
 NERF_TRAIN_N_STAGES = 5
 TRAIN_STAGES = ("rays_encode", "forward_gemm", "render_heads", "backward_gemm", "reduce_update")

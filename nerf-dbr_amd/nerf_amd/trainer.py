@@ -93,10 +93,12 @@ class MI355XTrainer:
         del kc, kf
         self._h = h
         self._loss = torch.zeros(3, dtype=torch.float32, device=self.device)
-        self._gen = None
+        self._grad_t = None
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
+            if getattr(self, "_grad_t", None) is not None:
+                self.lib.nerf_trainer_set_grad_buffer(self._h, None)   # before the tensor goes
             self.lib.nerf_trainer_destroy(self._h)
             self._h = ctypes.c_void_p()
 
@@ -116,10 +118,9 @@ class MI355XTrainer:
         t_rand = torch.rand(sel.numel(), self.n_coarse, device=self.device, generator=generator)
         return sel.to(torch.int32), t_rand
 
-    def train_step(self, batch: Mapping, select_inds=None, t_rand=None, update: bool = True,
-                   sync: bool = True):
-        """NeRFTrainer.train_step (trainer.py:83-138): returns the step's loss (a float, as
-        loss.item(); with sync=False the device tensor [loss, mse_coarse, mse_fine])."""
+    def _inputs(self, batch: Mapping, select_inds, t_rand):
+        """Device inputs of a step: image [H, W, 3], host pose [4, 4], focal, and the draws
+        (made here as the reference makes them when not injected)."""
         import torch
 
         image = batch["image"]
@@ -140,12 +141,20 @@ class MI355XTrainer:
             t_rand = t_draw if t_rand is None else t_rand
         sel = torch.as_tensor(select_inds).to(self.device, torch.int32).contiguous()
         tr = torch.as_tensor(t_rand).to(self.device, torch.float32).contiguous()
-        n = sel.numel()
-        if tuple(tr.shape) != (n, self.n_coarse):
-            raise ValueError(f"t_rand must be [{n}, {self.n_coarse}], got {tuple(tr.shape)}")
+        if tuple(tr.shape) != (sel.numel(), self.n_coarse):
+            raise ValueError(f"t_rand must be [{sel.numel()}, {self.n_coarse}], got {tuple(tr.shape)}")
+        return image, pose, focal, sel, tr
+
+    def train_step(self, batch: Mapping, select_inds=None, t_rand=None, update: bool = True,
+                   sync: bool = True):
+        """NeRFTrainer.train_step (trainer.py:83-138): returns the step's loss (a float, as
+        loss.item(); with sync=False the device tensor [loss, mse_coarse, mse_fine])."""
+        import torch
+
+        image, pose, focal, sel, tr = self._inputs(batch, select_inds, t_rand)
         stream = torch.cuda.current_stream(self.device)
-        rt._check(self.lib.nerf_train_step(self._h, image.data_ptr(), height, width, focal, rt._fptr(pose),
-                                           sel.data_ptr(), n, tr.data_ptr(),
+        rt._check(self.lib.nerf_train_step(self._h, image.data_ptr(), image.shape[0], image.shape[1], focal,
+                                           rt._fptr(pose), sel.data_ptr(), sel.numel(), tr.data_ptr(),
                                            0 if update else rt.NERF_TRAIN_NO_UPDATE, self._loss.data_ptr(),
                                            int(stream.cuda_stream)))
         # keep the inputs alive until the queued step has consumed them
@@ -153,6 +162,30 @@ class MI355XTrainer:
         if not sync:
             return self._loss
         return float(self._loss[0].item())
+
+    def backward(self, batch: Mapping, select_inds, t_rand, n_rays_total: int):
+        """This share's gradients of a step of n_rays_total rays (nerf_train_backward): the
+        data-parallel half step; returns the device loss parts [loss, mse_c, mse_f]."""
+        import torch
+
+        image, pose, focal, sel, tr = self._inputs(batch, select_inds, t_rand)
+        stream = torch.cuda.current_stream(self.device)
+        rt._check(self.lib.nerf_train_backward(self._h, image.data_ptr(), image.shape[0], image.shape[1], focal,
+                                               rt._fptr(pose), sel.data_ptr(), sel.numel(), int(n_rays_total),
+                                               tr.data_ptr(), self._loss.data_ptr(), int(stream.cuda_stream)))
+        self._keep = (image, sel, tr)
+        return self._loss
+
+    def grad_tensor(self):
+        """The gradient store as a device tensor [2 * NERF_TRAIN_NET_FLOATS] (coarse then fine,
+        state-dict order), so that torch.distributed can all-reduce it in place."""
+        import torch
+
+        if self._grad_t is None:
+            t = torch.zeros(2 * rt.NERF_TRAIN_NET_FLOATS, dtype=torch.float32, device=self.device)
+            rt._check(self.lib.nerf_trainer_set_grad_buffer(self._h, t.data_ptr()))
+            self._grad_t = t
+        return self._grad_t
 
     def update(self) -> None:
         """Clip + Adam + schedule on the current gradients (the last part of train_step)."""

@@ -411,6 +411,9 @@ def test_multi_rank_rehearsal_on_one_device():
     c4 = b["c4_hierarchical_sharded"]                 # config 4, every rank taking part
     assert c4["n_gpus"] == 2 and c4["rays_per_s"] > 0
     assert b["exchange_ms_per_frame"] > 0 and b["mlp_ms_per_frame_rank_max"] > 0
+    t = b["training"]                                 # data-parallel training step, every rank taking part
+    assert t["n_gpus"] == 2 and t["rays_per_s"] > 0 and t["parallelism"].startswith("data parallel x2")
+    assert t["loss_first_last"][-1] < t["loss_first_last"][0]
 
 
 def test_bench_single_gpu_json_contract():
@@ -442,6 +445,11 @@ def test_bench_single_gpu_json_contract():
     assert rf["traffic"] is None                      # PMC bytes are quoted for the headline frame only
     cb = b["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "rays/s" and cb["value"] > 0 and cb["cores"] >= 1
+    t = b["training"]                                 # the training-step leg
+    assert t["n_gpus"] == 1 and t["rays_per_s"] == pytest.approx(2048 / (t["ms_per_step"] * 1e-3), rel=1e-6)
+    assert 0 < t["gemm"]["frac"] < 1 and t["gemm"]["peak"] == 157.3
+    assert t["cpu_baseline"]["kind"] == "port" and t["cpu_baseline"]["value"] > 0
+    assert t["loss_first_last"][-1] < t["loss_first_last"][0]
 
 
 # ------------------------------------- compositing fused into the MLP epilogue --

@@ -194,3 +194,46 @@ def test_train_rejects_bad_select():
     gpu.train_step(batch, select_inds=sel, t_rand=np.zeros((8, 64), np.float32), update=False, sync=False)
     with pytest.raises(NerfError):
         gpu.grads(0)
+
+
+def test_train_backward_shares_sum_to_the_full_step(fx):
+    """Data parallelism on one GPU: three shares of the fixture step (nerf_train_backward with
+    the whole step's normalisation, gradients in caller-owned tensors) summed as the
+    all-reduce sums them equal the single-call step; the update on the summed gradients then
+    matches the single-call step's update.  Per sample the forward and backward-data GEMMs
+    are identical in either run (a row's result does not depend on the other rows), so no
+    ReLU flips: only the weight-gradient sums regroup (fp32 rounding level)."""
+    from nerf_amd.distributed import bands
+
+    n = int(fx["n_rays"])
+    sel, tr = fx["step0_select"].astype(np.int32), fx["step0_t_rand"]
+    full, _ = _trainer(n)
+    loss_full = full.train_step(_batch(fx), select_inds=sel, t_rand=tr, update=False, sync=False).cpu().numpy()
+    g_full = full.grad_tensor().cpu().numpy().astype(np.float64)
+    acc, loss = None, np.zeros(3)
+    for a, b in bands(3, n):
+        t, _ = _trainer(n)
+        g = t.grad_tensor()
+        loss += t.backward(_batch(fx), sel[a:b], tr[a:b], n_rays_total=n).cpu().numpy()
+        acc = g.clone() if acc is None else acc + g
+        last = t
+    assert np.allclose(loss, loss_full, rtol=1e-6, atol=0), (loss, loss_full)
+    g_sum = acc.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(g_sum - g_full) <= 1e-6 * np.linalg.norm(g_full)
+    off = 0
+    for net in (0, 1):
+        for k, shape in [(k, v.shape) for k, v in full.grads(net).items()]:
+            sz = int(np.prod(shape))
+            a, b = g_sum[off:off + sz], g_full[off:off + sz]
+            assert np.linalg.norm(a - b) <= 1e-5 * np.linalg.norm(b) + 1e-30, (net, k)
+            off += sz
+    # the update on the summed gradients (what every rank runs after the all-reduce)
+    last.grad_tensor().copy_(acc)
+    last.update()
+    full.update()
+    for net in (0, 1):
+        pa, pb = last.state_dicts()[net], full.state_dicts()[net]
+        for k in T.PARAM_ORDER:
+            d = np.abs(pa[k].astype(np.float64) - pb[k])
+            # Adam's first step is lr * sign(g): equal except where g sits at rounding level
+            assert np.mean(d <= 1e-7 + 1e-6 * np.abs(pb[k])) >= 0.999, (net, k)

@@ -178,6 +178,77 @@ def test_band_gather_gloo_world2(height):
             assert root is None
 
 
+class _FakeTrainer:
+    """A linear stand-in for MI355XTrainer: a share's 'gradient' is sum over its rays of
+    g(ray) / n_total, so the all-reduced sum must equal the single-rank full step."""
+
+    def __init__(self):
+        import torch
+
+        self.g = torch.zeros(6, dtype=torch.float64)
+        self.loss = torch.zeros(3, dtype=torch.float64)
+        self.updates = 0
+
+    def grad_tensor(self):
+        return self.g
+
+    def backward(self, batch, select, t_rand, n_rays_total):
+        import torch
+
+        feat = torch.stack([select.double(), t_rand.double().sum(1), select.double() ** 2,
+                            torch.ones_like(select.double()), t_rand.double()[:, 0], select.double() % 7], 1)
+        self.g.copy_(feat.sum(0) / n_rays_total)
+        self.loss.copy_(torch.tensor([1.0, 2.0, 3.0], dtype=torch.float64) * select.numel() / n_rays_total)
+        return self.loss
+
+    def update(self):
+        self.updates += 1
+
+
+def _train_worker(rank, world, port, n, q):
+    import torch
+    import torch.distributed as dist
+
+    from nerf_amd import distributed as D
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    gen = torch.Generator().manual_seed(11)        # the same step draw on every rank
+    select = torch.randperm(4096, generator=gen)[:n]
+    t_rand = torch.rand(n, 4, generator=gen)
+    tr = _FakeTrainer()
+    loss = D.train_step_sharded(tr, None, select, t_rand)
+    full = _FakeTrainer()
+    full.backward(None, select, t_rand, n)
+    q.put((rank, tr.g.numpy().copy(), loss.numpy().copy(), full.g.numpy().copy(), tr.updates))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [37, 2048])
+def test_train_step_sharded_gloo_world2(n):
+    """Data-parallel training step: shares, loss normalisation and the gradient all-reduce."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, g, loss, full, updates in outs:
+        assert np.allclose(g, full, rtol=1e-12, atol=0), rank      # reduced share sums == the full step
+        assert np.allclose(loss, [1.0, 2.0, 3.0], rtol=1e-12), rank
+        assert updates == 1
+
+
 # ---------------------------------------- plugin interface vs the reference --
 def _sig_fixture():
     import json
