@@ -6,20 +6,19 @@
 // clip_grad_norm_, optim.Adam and ExponentialLR.
 //
 // Structure of one step (both nets, one stream, no host synchronisation):
-//   rays of the selected pixels -> per net: samples + encodings -> 9 forward GEMMs
-//   (8 trunk layers, then the colour-0 layer and the density head as ONE GEMM of 129
-//   output columns: both read the trunk output) -> colour-1 + sigmoid -> volume render
-//   forward + MSE + its backward per ray -> head backward -> backward GEMMs (weight
-//   gradients as split-K partials over samples, data gradients with the ReLU mask in
-//   the epilogue) -> one reduction into the flat gradients -> grad norm, clip, Adam,
-//   and the relayout of the updated weights into the GEMM operand layouts.
+//   rays of the selected pixels -> per net: samples + encodings (rows for the weight
+//   gradients) -> the whole forward in ONE register-stationary launch (mlp_f32.hip's
+//   shape: activations stay in registers from layer to layer; each layer's rows and ReLU
+//   bits are written for the backward) -> volume render forward + MSE + its backward per
+//   ray -> head backward -> backward GEMMs (data gradients with the ReLU bits in the
+//   epilogue, weight gradients as split-K partials over the samples) -> one reduction into
+//   the flat gradients -> grad norm, clip, Adam, and the relayout of the updated weights.
 //
 // GEMM: C[M][N] = A[M][K] . B[K][N] on v_mfma_f32_32x32x2_f32 (exact fp32 fma chains),
-// 128x128 tiles per 256-thread workgroup, 16-deep k tiles double-buffered through LDS.
-// Activations are [sample][feature] row-major, so the three GEMM kinds are
-//   forward      A = X  [P][in]  (k contiguous)   B = W^T [in][out]
-//   backward-data A = dZ [P][out] (k contiguous)  B = W   [out][in]
-//   weight grad  A = dZ^T (m contiguous: dZ rows)  B = X   [P][in]   (K = samples, split)
+// 128x128 tiles per 256-thread workgroup, 16-deep k tiles double-buffered through LDS and
+// staged two ahead in registers.  Activations are [sample][feature] row-major, so
+//   backward-data A = dZ [P][out] (k contiguous)   B = W   [out][in]
+//   weight grad   A = dZ^T (m contiguous: dZ rows) B = X   [P][in]   (K = samples, split)
 // and every B is [K][N] with n contiguous.
 #include <cmath>
 #include <cstring>
@@ -85,40 +84,29 @@ constexpr long kFC1W = tensor_desc(20).off, kFC1B = tensor_desc(21).off;
 
 constexpr int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-// GEMM operand copies of one net's weights, rewritten after every update:
-//   Wt_l  [round16(in_l)][256]  trunk layer l transposed (forward B), zero rows past in_l
-//   WtH   [288][132]  head (colour-0 and density) transposed: column n < 128 = colour-0
-//                     row n, column 128 = density (zero for the direction inputs)
+// Operand copies of one net's weights, rewritten after every update (relayout_kernel):
 //   W4h   [256][256]  layers.4 weight's hidden columns (backward-data B; the flat
 //                     tensor's 319-float rows are not 16-B aligned)
-//   WcH   [144][256]  head rows (colour-0 rows, then density) over the hidden inputs
-//   bH    [132]       head bias (colour-0, density, zeros)
+//   WcH   [144][256]  the head's rows over the hidden inputs: colour-0 rows, then the
+//                     density row, then zeros (backward-data B of the head, K = 129)
+//   F32   the f32 MFMA blob of mlp_f32.hip (nerf_layout.h: per layer [u/4][tile][lane][4]),
+//         read by the fused forward kernel
+//   PRM   the params blob (biases in accumulator order, density and colour-1 rows)
 constexpr int kHeadN = kC0 + 1, kHeadLd = 132, kHeadK = kH + kDirDim;   // 129, 132, 283
-constexpr long wt_off(int l) {
-  long o = 0;
-  for (int j = 0; j < l; ++j) o += long(round_up(kTrunkIn[j], 16)) * kH;
-  return o;
-}
-constexpr long kWtH = wt_off(8);
-constexpr long kW4h = kWtH + long(round_up(kHeadK, 16)) * kHeadLd;
+constexpr long kW4h = 0;
 constexpr long kWcH = kW4h + long(kH) * kH;
-constexpr long kBH = kWcH + 144L * kH;
-constexpr long kGemmFloats = round_up(int(kBH + kHeadLd), 64);
+constexpr long kF32Blob = round_up(int(kWcH + 144L * kH), 64);
+constexpr long kPrmBlob = kF32Blob + round_up(f32_blob_floats(), 64);
+constexpr long kGemmFloats = kPrmBlob + round_up(kParamFloats, 64);
 
 // Per-sample activation workspace (floats per sample; each array [P][ld])
 constexpr int kPeLd = 64, kDpeLd = 28;
 
-#ifndef NERF_TRAIN_BK
-#define NERF_TRAIN_BK 16
-#endif
-#ifndef NERF_TRAIN_SKCHUNK
-#define NERF_TRAIN_SKCHUNK 256   // samples per block of the skinny weight-gradient kernel
-#endif
-#ifndef NERF_TRAIN_PF
-#define NERF_TRAIN_PF 2   // k tiles staged ahead in registers (1 or 2)
-#endif
-constexpr int BM = 128, BN = 128, BK = NERF_TRAIN_BK, LDT = 132;   // LDS row stride (floats)
+// 16-deep k tiles (32: two workgroups per CU instead of three, +11 % step time)
+constexpr int BM = 128, BN = 128, BK = 16, LDT = 132;   // LDS row stride (floats)
 constexpr int kLd = BK / 8;   // float4 loads per thread per operand and k tile (256 threads)
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ GEMM --
 struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 % 4 == 0)
@@ -127,17 +115,15 @@ struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 %
   int ld1 = 0, ld2 = 0, w1 = 0x7fffffff;
 };
 
-enum Epi { kEpiBiasRelu = 0, kEpiMask = 1, kEpiPartial = 2 };
+enum Epi { kEpiMask = 1, kEpiPartial = 2 };
 
 struct GemmArgs {
   int M = 0, N = 0, K = 0;
   Src2 a, b;
   float* c = nullptr;
   int ldc = 0;
-  const float* bias = nullptr;      // kEpiBiasRelu: per column
   const unsigned* mask = nullptr;   // kEpiMask: C = acc where the ReLU bit of (m, n) is set, else 0
-  unsigned* bits = nullptr;         // kEpiBiasRelu (optional): ReLU bits of C, [M][N / 32] words
-  int ldm = 0;                      // words per row of mask / bits
+  int ldm = 0;                      // words per row of mask
   float* bias_part = nullptr;       // kEpiPartial: [split][M] sums of A over the split's k
   int k_split = 0;                  // kEpiPartial: k range per blockIdx.z (multiple of BK)
   long c_split = 0;                 // kEpiPartial: floats per split partial
@@ -264,22 +250,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     store_a<kAK>(As[buf], t, ra);
     store_b(Bs[buf], t, rb);
   };
-#if NERF_TRAIN_PF == 1
-  f32x4 ra[kLd], rb[kLd];
-  if (nt > 0) {
-    load_tile(0, ra, rb);
-    store_tile(0, ra, rb);
-    __syncthreads();
-  }
-  for (int it = 0; it < nt; ++it) {
-    const int cur = it & 1;
-    const bool more = it + 1 < nt;
-    if (more) load_tile(it + 1, ra, rb);
-    gemm_tile<kEpi>(As[cur], Bs[cur], acc, bsum, wm, wn, h, l32, t);
-    if (more) store_tile(cur ^ 1, ra, rb);
-    __syncthreads();
-  }
-#else
   // k tiles staged two ahead: registers hold tile it+1 (landing) and tile it+2 (issued
   // this iteration) while LDS buffer it&1 is consumed; the register sets alternate by
   // iteration parity, so the loop is unrolled by two
@@ -302,7 +272,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     __syncthreads();
   }
   if (it < nt) gemm_tile<kEpi>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);   // odd tile count: the last
-#endif
   float* c = g.c + (kEpi == kEpiPartial ? long(blockIdx.z) * g.c_split : 0L);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -311,24 +280,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
       const int n = n0 + wn * 64 + j * 32 + l32;
       const bool nok = n < g.N;
       const int word = (n0 + wn * 64 + j * 32) >> 5;   // this 32-column group's word in a row
-      const float bn = kEpi == kEpiBiasRelu && nok ? g.bias[n] : 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
         const bool ok = nok && m < g.M;
         float v = acc[i][j][r];
-        if (kEpi == kEpiBiasRelu) {
-          v = relu(__fadd_rn(v, bn));
-          if (g.bits) {
-            // ReLU bits for the backward pass (1 bit instead of the 4-B activation):
-            // lanes 0-31 are row acc_row(r, 0), lanes 32-63 row acc_row(r, 1)
-            const unsigned long long bal = __ballot(ok && v > 0.0f);
-            if (l32 == 0 && m < g.M) g.bits[long(m) * g.ldm + word] = unsigned(h ? bal >> 32 : bal);
-          }
-        }
-#ifndef NERF_TRAIN_ABLATE_MASK
         if (kEpi == kEpiMask && ok) v = (g.mask[long(m) * g.ldm + word] >> l32) & 1u ? v : 0.0f;
-#endif
         if (ok) c[long(m) * g.ldc + n] = v;
       }
     }
@@ -406,26 +363,6 @@ __global__ void train_encode_kernel(const float* __restrict__ rays_o, const floa
   f32x4* du = (f32x4*)(dpe + p * kDpeLd);
 #pragma unroll
   for (int q = 0; q < kDpeLd / 4; ++q) du[q] = f32x4{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]};
-}
-
-// colour-1 + sigmoid (nerf.py:123-129) per sample; the density is column 128 of
-// the head GEMM's output.  rgbs[p] = (r, g, b, sigma).
-__global__ void color_out_kernel(const float* __restrict__ hc, const float* __restrict__ prm, long n_points,
-                                 f32x4* __restrict__ rgbs) {
-  const long p = long(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= n_points) return;
-  const float* row = hc + p * kHeadLd;
-  const float* w1 = prm + kFC1W;
-  float acc[3] = {0.0f, 0.0f, 0.0f};
-  for (int j = 0; j < kC0; j += 4) {
-    const f32x4 v = ld4(row + j);
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[c] = fmaf(v[q], w1[c * kC0 + j + q], acc[c]);
-  }
-  rgbs[p] = f32x4{sigmoid_ref(__fadd_rn(acc[0], prm[kFC1B])), sigmoid_ref(__fadd_rn(acc[1], prm[kFC1B + 1])),
-                  sigmoid_ref(__fadd_rn(acc[2], prm[kFC1B + 2])), row[kC0]};
 }
 
 // volume_render (rendering.py:102-143) forward, the MSE term of this ray, and the
@@ -518,6 +455,146 @@ __global__ void head_bwd_kernel(const float* __restrict__ hc, const f32x4* __res
     o[0] = d[3];
   }
   *(f32x4*)(dhc + p * kHeadLd + n) = o;
+}
+
+// ------------------------------------------------------- fused forward --
+// The forward of one net in one launch, in mlp_f32.hip's register-stationary shape
+// (4 waves x 32 samples, one wave per SIMD, H^T = W . X^T with the accumulator of a
+// layer as the next layer's B operand, A fragments read as float4 from the f32 blob
+// in L2), plus what the backward needs: every trunk layer's post-ReLU rows [P][256]
+// and its ReLU bits [P][8] words, the colour-0 output and the density [P][132],
+// and (r, g, b, sigma) per sample.  Same numerics as the parity render path.
+template <int L>
+constexpr int f32_layer_offset_t() {
+  int off = 0;
+  for (int l = 0; l < L; ++l) off += f32_layer_floats(l);
+  return off;
+}
+
+// prev_row (optional): where the previous layer's activations (this layer's B operand,
+// live in registers anyway) go as a row of this lane's sample; one 16-B piece is
+// stored after each k-step group's weight loads are issued, so no weight load of this
+// layer waits behind more than one store (vmcnt counts loads and stores in issue order).
+template <int L, int NT, int NEXT>
+__device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)[8], const float (&ext)[NEXT],
+                                          const f32x4* __restrict__ blob, const float* __restrict__ prm, int lane,
+                                          int h, float* __restrict__ prev_row = nullptr) {
+  constexpr LayerShape sh = layer_shape(L);
+  constexpr int KH = sh.hidden / 2;
+  constexpr int KU = ksteps_f32(L);
+  static_assert(KU == KH + (sh.extra == kNone ? 0 : NEXT), "layer/ext mismatch");
+  load_bias<NT>(acc, prm, L, h);
+  const f32x4* a_base = blob + f32_layer_offset_t<L>() / 4 + lane;
+#pragma unroll
+  for (int ug = 0; ug < KU / 4; ++ug) {
+    f32x4 a[NT];
+#pragma unroll
+    for (int o = 0; o < NT; ++o) a[o] = a_base[(ug * NT + o) * 64];
+    if (KH > 0 && ug < KH / 4 && prev_row != nullptr) {
+      const int t = ug >> 2, j = ug & 3;
+      *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
+          f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = 4 * ug + i;
+      const float b = u < KH ? prev[u >> 4][u & 15] : ext[u - KH];
+#pragma unroll
+      for (int o = 0; o < NT; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[o][i], b, acc[o], 0, 0, 0);
+    }
+  }
+}
+
+// Rows of this lane's sample: register 4j..4j+3 of tile t are features 32t + 8j + 4h + 0..3.
+template <int NT>
+__device__ __forceinline__ void store_rows(const f32x16 (&a)[8], float* __restrict__ row, int h) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *(f32x4*)(row + 32 * t + 8 * j + 4 * h) = f32x4{a[t][4 * j], a[t][4 * j + 1], a[t][4 * j + 2], a[t][4 * j + 3]};
+}
+
+// ReLU bits of this lane's sample, one word per 32 features (bit = feature % 32): each
+// lane half holds 16 of a tile's 32 rows; the halves' masks meet by a cross-half swap.
+__device__ __forceinline__ void store_bits(const f32x16 (&a)[8], unsigned* __restrict__ words, int h, bool store) {
+  unsigned w[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    unsigned m = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m |= (a[t][r] > 0.0f ? 1u : 0u) << acc_row(r, h);
+    const auto sw = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+    w[t] = unsigned(sw[0]) | unsigned(sw[1]);
+  }
+  if (store) {
+    ((u32x4_t*)words)[0] = u32x4_t{w[0], w[1], w[2], w[3]};
+    ((u32x4_t*)words)[1] = u32x4_t{w[4], w[5], w[6], w[7]};
+  }
+}
+
+struct FwdOut {
+  float* h[8];
+  unsigned* mb[8];
+  float* hc;
+  f32x4* rgbs;
+};
+
+__global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restrict__ blob,
+                                                           const float* __restrict__ prm, SampleSrc src, long n_points,
+                                                           FwdOut o) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const long p = (long(blockIdx.x) * 4 + wave) * kSamplesPerWave + (lane & 31);
+  const bool valid = p < n_points;
+  const long pc = valid ? p : n_points - 1;
+  float x[3], d[3];
+  fetch_sample<false>(src, pc, x, d);
+  float pe[32], de[16];
+  pos_encode(x[0], x[1], x[2], h, pe);
+  dir_encode(d[0], d[1], d[2], h, de);
+  f32x16 a[8], b[8];
+  // each layer's rows are stored while the next layer runs (fwd_layer prev_row); bits now
+  float* const nul = nullptr;
+#define ROW(l) (valid ? o.h[l] + p * kH : nul)
+#define BITS(acc, l) store_bits(acc, o.mb[l] + p * (kH / 32), h, valid && h == 0)
+  fwd_layer<L0, 8, 32>(a, b, pe, blob, prm, lane, h);
+  relu_tiles<8>(a);
+  BITS(a, 0);
+  fwd_layer<L1, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(0));
+  relu_tiles<8>(b);
+  BITS(b, 1);
+  fwd_layer<L2, 8, 32>(a, b, pe, blob, prm, lane, h, ROW(1));
+  relu_tiles<8>(a);
+  BITS(a, 2);
+  fwd_layer<L3, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(2));
+  relu_tiles<8>(b);
+  BITS(b, 3);
+  fwd_layer<L4, 8, 32>(a, b, pe, blob, prm, lane, h, ROW(3));   // skip: [x, pe] (nerf.py:109-110)
+  relu_tiles<8>(a);
+  BITS(a, 4);
+  fwd_layer<L5, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(4));
+  relu_tiles<8>(b);
+  BITS(b, 5);
+  fwd_layer<L6, 8, 32>(a, b, pe, blob, prm, lane, h, ROW(5));
+  relu_tiles<8>(a);
+  BITS(a, 6);
+  fwd_layer<L7, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(6));
+  relu_tiles<8>(b);
+  BITS(b, 7);
+  const float sigma = density_head(b, prm, h);
+  fwd_layer<C0, 4, 16>(a, b, de, blob, prm, lane, h, ROW(7));   // [x, PE4(d)] (nerf.py:117-121)
+#undef ROW
+#undef BITS
+  relu_tiles<4>(a);
+  if (valid) store_rows<4>(a, o.hc + p * kHeadLd, h);
+  float rgb[3];
+  color_head(a, prm, h, rgb);
+  if (valid && h == 0) {
+    o.hc[p * kHeadLd + kC0] = sigma;
+    o.rgbs[p] = f32x4{rgb[0], rgb[1], rgb[2], sigma};
+  }
 }
 
 // --------------------------------------------------- gradient reduction --
@@ -704,30 +781,41 @@ __global__ void relayout_kernel(const float* __restrict__ params, float* __restr
   const float* prm = params + blockIdx.y * kNetFloats;
   float* out = gemmw + blockIdx.y * kGemmFloats;
   float v = 0.0f;
-  if (e < kWtH) {
-    int l = 0;
-    while (l < 7 && e >= wt_off(l + 1)) ++l;
-    const long o = e - wt_off(l);
-    const int k = int(o / kH), n = int(o - long(k) * kH);
-    if (k < kTrunkIn[l]) v = prm[w_off(l) + long(n) * kTrunkIn[l] + k];
-  } else if (e < kW4h) {
-    const long o = e - kWtH;
-    const int k = int(o / kHeadLd), n = int(o - long(k) * kHeadLd);
-    if (k < kHeadK && n < kC0) v = prm[kFC0W + long(n) * kHeadK + k];
-    else if (k < kH && n == kC0) v = prm[kFDensW + k];
-  } else if (e < kWcH) {
+  if (e < kWcH) {
     const long o = e - kW4h;
     const int n = int(o / kH), k = int(o - long(n) * kH);
     v = prm[w_off(4) + long(n) * kTrunkIn[4] + k];
-  } else if (e < kBH) {
+  } else if (e < kWcH + 144L * kH) {
     const long o = e - kWcH;
     const int n = int(o / kH), k = int(o - long(n) * kH);
     if (n < kC0) v = prm[kFC0W + long(n) * kHeadK + k];
     else if (n == kC0) v = prm[kFDensW + k];
-  } else if (e < kBH + kHeadLd) {
-    const int n = int(e - kBH);
-    if (n < kC0) v = prm[kFC0B + n];
-    else if (n == kC0) v = prm[kFDensB];
+  } else if (e >= kF32Blob && e < kF32Blob + f32_blob_floats()) {
+    // pack.cpp's f32 blob, element by element: layer l, k-step group ug, tile o, lane, i
+    long o = e - kF32Blob;
+    int l = 0;
+    while (l < kNumMfmaLayers - 1 && o >= f32_layer_floats(l)) o -= f32_layer_floats(l++);
+    const int nt = out_tiles(l);
+    const int i = int(o & 3), lane = int((o >> 2) & 63), tile = int((o >> 8) % nt), ug = int((o >> 8) / nt);
+    const int row = 32 * tile + (lane & 31), col = f32_k_col(l, 4 * ug + i, lane >> 5);
+    if (col >= 0) v = l == C0 ? prm[kFC0W + long(row) * kHeadK + col] : prm[w_off(l) + long(row) * kTrunkIn[l] + col];
+  } else if (e >= kPrmBlob && e < kPrmBlob + kParamFloats) {
+    const int q = int(e - kPrmBlob);
+    if (q < kSigW) {                       // bias[l][tile][h][r]
+      const int l = q / 256, rem = q % 256, tile = rem / 32, hh = (rem / 16) & 1, r = rem & 15;
+      const int row = 32 * tile + acc_row(r, hh);
+      if (tile < out_tiles(l)) v = l == C0 ? prm[kFC0B + row] : prm[b_off(l) + row];
+    } else if (q < kSigB) {                // density weight [h][t][r]
+      const int rem = q - kSigW, hh = rem / 128, t = (rem / 16) & 7, r = rem & 15;
+      v = prm[kFDensW + 32 * t + acc_row(r, hh)];
+    } else if (q == kSigB) {
+      v = prm[kFDensB];
+    } else if (q >= kC1W && q < kC1B) {    // colour-1 weight [c][h][t][r]
+      const int rem = q - kC1W, c = rem / 128, hh = (rem / 64) & 1, t = (rem / 16) & 3, r = rem & 15;
+      v = prm[kFC1W + c * kC0 + 32 * t + acc_row(r, hh)];
+    } else if (q >= kC1B && q < kC1B + 3) {
+      v = prm[kFC1B + (q - kC1B)];
+    }
   }
   out[e] = v;
 }
@@ -888,32 +976,18 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   if ((rc = mark(1)) != NERF_OK) return rc;
 
   // forward (nerf.py:104-121)
-  for (int l = 0; l < 8; ++l) {
-    GemmArgs g;
-    g.M = int(P), g.N = kH, g.K = kTrunkIn[l];
-    if (l == 0) g.a = Src2{a.pe, nullptr, kPeLd, 0, 0x7fffffff};
-    else if (l == 4) g.a = Src2{a.h[3], a.pe, kH, kPeLd, kH};
-    else g.a = Src2{a.h[l - 1], nullptr, kH, 0, 0x7fffffff};
-    g.b = Src2{gw + wt_off(l), nullptr, kH, 0, 0x7fffffff};
-    g.c = a.h[l], g.ldc = kH;
-    g.bias = prm + b_off(l);
-    g.bits = a.mb[l], g.ldm = kH / 32;
-    HIP_TRY((gemm<true, kEpiBiasRelu>(g, 1, s)));
-  }
   {
-    GemmArgs g;
-    g.M = int(P), g.N = kHeadN, g.K = kHeadK;
-    g.a = Src2{a.h[7], a.dpe, kH, kDpeLd, kH};
-    g.b = Src2{gw + kWtH, nullptr, kHeadLd, 0, 0x7fffffff};
-    g.c = a.hc, g.ldc = kHeadLd;
-    g.bias = gw + kBH;
-    HIP_TRY((gemm<true, kEpiBiasRelu>(g, 1, s)));
+    FwdOut fo;
+    for (int l = 0; l < 8; ++l) fo.h[l] = a.h[l], fo.mb[l] = a.mb[l];
+    fo.hc = a.hc;
+    fo.rgbs = (f32x4*)a.rgbs;
+    SampleSrc src{rays_o, rays_d, z, z_stride, S, nullptr, nullptr};
+    hipLaunchKernelGGL(train_fwd_kernel, dim3(blocks_for(P, 4 * kSamplesPerWave)), dim3(256), 0, s,
+                       (const f32x4*)(gw + kF32Blob), gw + kPrmBlob, src, P, fo);
+    HIP_TRY(hipGetLastError());
   }
   if ((rc = mark(2)) != NERF_OK) return rc;
-
-  // colour head, volume render + loss, their backward (rendering.py:102-143, trainer.py:117-126)
-  hipLaunchKernelGGL(color_out_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, a.hc, prm, P, (f32x4*)a.rgbs);
-  HIP_TRY(hipGetLastError());
+  // volume render + loss, their backward (rendering.py:102-143, trainer.py:117-126)
   const float gnorm = float(2.0 / (3.0 * n_total));   // mse_loss backward over the whole step's rays
   hipLaunchKernelGGL(render_train_kernel, dim3(blocks_for(n_rays, 64)), dim3(64), 0, s, (const f32x4*)a.rgbs, z,
                      z_stride, rays_d, target, n_rays, S, gnorm, a.tb, (f32x4*)a.dpre, loss_ray);
@@ -925,7 +999,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
 
   // backward GEMMs; weight gradients as split partials
   size_t cur = 0;
-  constexpr int kSkinnyChunk = NERF_TRAIN_SKCHUNK;
+  constexpr int kSkinnyChunk = 256;   // samples per block of the skinny weight-gradient kernel
   const int sk_splits = int(blocks_for(P, kSkinnyChunk));
   WJob jc1{3, kC0, sk_splits, kSkinnyChunk, 0, 0}, jd{1, kH, sk_splits, kSkinnyChunk, 0, 0};
   for (WJob* j : {&jc1, &jd}) {

