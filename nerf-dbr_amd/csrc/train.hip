@@ -10,16 +10,10 @@
 //   gradients) -> the whole forward in ONE register-stationary launch (mlp_f32.hip's
 //   shape: activations stay in registers from layer to layer; each layer's rows and ReLU
 //   bits are written for the backward) -> volume render forward + MSE + its backward per
-//   ray -> head backward -> backward GEMMs (data gradients with the ReLU bits in the
-//   epilogue, weight gradients as split-K partials over the samples) -> one reduction into
-//   the flat gradients -> grad norm, clip, Adam, and the relayout of the updated weights.
-//
-// GEMM: C[M][N] = A[M][K] . B[K][N] on v_mfma_f32_32x32x2_f32 (exact fp32 fma chains),
-// 128x128 tiles per 256-thread workgroup, 16-deep k tiles double-buffered through LDS and
-// staged two ahead in registers.  Activations are [sample][feature] row-major, so
-//   backward-data A = dZ [P][out] (k contiguous)   B = W   [out][in]
-//   weight grad   A = dZ^T (m contiguous: dZ rows) B = X   [P][in]   (K = samples, split)
-// and every B is [K][N] with n contiguous.
+//   ray -> head backward -> the whole backward-data chain in ONE launch of the same shape
+//   run backwards (dZ of every layer written) -> weight gradients as split-K GEMM partials
+//   over the samples -> one reduction into the flat gradients -> grad norm, clip, Adam,
+//   and the relayout of the updated weights into the two kernels' fragment blobs.
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -85,175 +79,162 @@ constexpr long kFC1W = tensor_desc(20).off, kFC1B = tensor_desc(21).off;
 constexpr int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 // Operand copies of one net's weights, rewritten after every update (relayout_kernel):
-//   W4h   [256][256]  layers.4 weight's hidden columns (backward-data B; the flat
-//                     tensor's 319-float rows are not 16-B aligned)
-//   WcH   [144][256]  the head's rows over the hidden inputs: colour-0 rows, then the
-//                     density row, then zeros (backward-data B of the head, K = 129)
 //   F32   the f32 MFMA blob of mlp_f32.hip (nerf_layout.h: per layer [u/4][tile][lane][4]),
 //         read by the fused forward kernel
 //   PRM   the params blob (biases in accumulator order, density and colour-1 rows)
-constexpr int kHeadN = kC0 + 1, kHeadLd = 132, kHeadK = kH + kDirDim;   // 129, 132, 283
-constexpr long kW4h = 0;
-constexpr long kWcH = kW4h + long(kH) * kH;
-constexpr long kF32Blob = round_up(int(kWcH + 144L * kH), 64);
+constexpr int kHeadLd = 132, kHeadK = kH + kDirDim;   // head rows [P][132]; colour-0 inputs 283
+constexpr long kF32Blob = 0;
 constexpr long kPrmBlob = kF32Blob + round_up(f32_blob_floats(), 64);
-constexpr long kGemmFloats = kPrmBlob + round_up(kParamFloats, 64);
+//   BWD   the transposed weights for the fused backward-data chain (train_bwd_kernel), in
+//         the forward blob's fragment order: per backward layer b (0 the head, then layers
+//         7..1) [u/4][tile][lane][4], A[row = input feature][k-step u, half h] =
+//         W[output feature hid_f32_feature(u, h)][input]; the head's k runs over the 128
+//         colour-0 rows, then one k-step for the density row (half 0), zero-padded to 68
+constexpr int kBwdLayers = 8;
+constexpr int kHeadBwdKsteps = 68;
+constexpr int bwd_ksteps(int b) { return b == 0 ? kHeadBwdKsteps : kH / 2; }
+constexpr int bwd_layer_floats(int b) { return bwd_ksteps(b) * 8 * 64; }
+constexpr long bwd_layer_offset(int b) {
+  long o = 0;
+  for (int i = 0; i < b; ++i) o += bwd_layer_floats(i);
+  return o;
+}
+constexpr int bwd_trunk_layer(int b) { return 8 - b; }   // b = 1..7 -> layers 7..1
+constexpr long kBwdBlob = kPrmBlob + round_up(kParamFloats, 64);
+constexpr long kGemmFloats = kBwdBlob + round_up(int(bwd_layer_offset(kBwdLayers)), 64);
 
 // Per-sample activation workspace (floats per sample; each array [P][ld])
 constexpr int kPeLd = 64, kDpeLd = 28;
 
-// 16-deep k tiles (32: two workgroups per CU instead of three, +11 % step time)
-constexpr int BM = 128, BN = 128, BK = 16, LDT = 132;   // LDS row stride (floats)
-constexpr int kLd = BK / 8;   // float4 loads per thread per operand and k tile (256 threads)
+// 16-deep k tiles (32 with 128x128 tiles: two workgroups per CU instead of three, +11 %)
+constexpr int BK = 16;
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
-// ------------------------------------------------------------------ GEMM --
+// ------------------------------------------------------- weight gradients --
+// Partial weight gradients dW[m][n] = sum_k dZ[k][m] X[k][n] over one split of the samples
+// (k), on v_mfma_f32_32x32x2_f32: 256x256 tiles per 512-thread workgroup (8 waves x 64x128)
+// for the 256-wide layers, whose operands are then read once, 128x128 per 256 threads
+// (4 waves x 64x64) for the others; 16-deep k tiles double-buffered through LDS and
+// staged two ahead in registers.  Both operands are sample rows with the tile's 128 columns contiguous, so
+// every load is a float4 of a row and lands in LDS as is.  The first column tile also sums
+// dZ over k for its rows (the bias gradient).
 struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 % 4 == 0)
   const float* p1 = nullptr;
   const float* p2 = nullptr;
   int ld1 = 0, ld2 = 0, w1 = 0x7fffffff;
 };
 
-enum Epi { kEpiMask = 1, kEpiPartial = 2 };
-
 struct GemmArgs {
   int M = 0, N = 0, K = 0;
-  Src2 a, b;
-  float* c = nullptr;
+  Src2 a, b;                        // A: dZ rows (a.p1, [K][a.ld1]); B: X rows, two sources
+  float* c = nullptr;               // [split][M][ldc]
   int ldc = 0;
-  const unsigned* mask = nullptr;   // kEpiMask: C = acc where the ReLU bit of (m, n) is set, else 0
-  int ldm = 0;                      // words per row of mask
-  float* bias_part = nullptr;       // kEpiPartial: [split][M] sums of A over the split's k
-  int k_split = 0;                  // kEpiPartial: k range per blockIdx.z (multiple of BK)
-  long c_split = 0;                 // kEpiPartial: floats per split partial
+  float* bias_part = nullptr;       // [split][M] sums of A over the split's k
+  int k_split = 0;                  // k range per blockIdx.z (multiple of BK)
+  long c_split = 0;                 // floats per split partial
 };
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 
-// One thread's two float4 of a BMxBK A tile (rows m0.., k0..).  Sources hold at
-// least round_up4(width) valid floats per row; elements past M/K are zero.
-template <bool kAK>
-__device__ __forceinline__ void load_a(const GemmArgs& g, int m0, int k0, int t, f32x4 (&ra)[kLd]) {
-#pragma unroll
-  for (int i = 0; i < kLd; ++i) {
-    const int idx = t + 256 * i;
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (kAK) {
-      const int m = m0 + idx / (BK / 4), k = k0 + 4 * (idx % (BK / 4));
-      if (m < g.M && k < g.K) {
-        v = k < g.a.w1 ? ld4(g.a.p1 + long(m) * g.a.ld1 + k) : ld4(g.a.p2 + long(m) * g.a.ld2 + (k - g.a.w1));
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (k + j >= g.K) v[j] = 0.0f;
-      }
-    } else {
-      const int k = k0 + (idx >> 5), m = m0 + 4 * (idx & 31);
-      if (k < g.K && m < g.M) {
-        v = ld4(g.a.p1 + long(k) * g.a.ld1 + m);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (m + j >= g.M) v[j] = 0.0f;
-      }
-    }
-    ra[i] = v;
-  }
-}
+// Workgroup tile BMT x BNT over WAVES waves, each wave 64 rows x (BNT / WN) columns.
+template <int BMT, int BNT, int WAVES>
+struct WTile {
+  static constexpr int kThreads = 64 * WAVES;
+  static constexpr int kWM = BMT / 64, kWN = WAVES / kWM;
+  static constexpr int kTN = BNT / kWN / 32;                 // 32-column MFMA tiles per wave
+  static constexpr int kLdA = BK * BMT / 4 / kThreads;       // float4 per thread per k tile
+  static constexpr int kLdB = BK * BNT / 4 / kThreads;
+  static constexpr int kPitchA = BMT + 4, kPitchB = BNT + 4; // LDS row pitches (floats)
+  static_assert(kWM * kWN == WAVES && kTN >= 1 && kLdA >= 1 && kLdB >= 1, "tile geometry");
+};
 
-template <bool kAK>
-__device__ __forceinline__ void store_a(float* as, int t, const f32x4 (&ra)[kLd]) {
+// A thread's float4 pieces of a BK x C tile (columns c0.., rows k0..): sources hold at
+// least round_up4(width) valid floats per row; elements past the width or K are zero.
+template <int C, int THREADS, int NLD>
+__device__ __forceinline__ void load_rows(const Src2& src, int width, int K, int c0, int k0, int t,
+                                          f32x4 (&r)[NLD]) {
 #pragma unroll
-  for (int i = 0; i < kLd; ++i) {
-    const int idx = t + 256 * i;
-    if (kAK) {
-      const int m = idx / (BK / 4), q = idx % (BK / 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) as[(4 * q + j) * LDT + m] = ra[i][j];
-    } else {
-      *(f32x4*)(as + (idx >> 5) * LDT + 4 * (idx & 31)) = ra[i];
-    }
-  }
-}
-
-__device__ __forceinline__ void load_b(const GemmArgs& g, int n0, int k0, int t, f32x4 (&rb)[kLd]) {
-#pragma unroll
-  for (int i = 0; i < kLd; ++i) {
-    const int idx = t + 256 * i;
-    const int k = k0 + (idx >> 5), n = n0 + 4 * (idx & 31);
+  for (int i = 0; i < NLD; ++i) {
+    const int idx = t + THREADS * i;
+    const int k = k0 + idx / (C / 4), c = c0 + 4 * (idx % (C / 4));
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (k < g.K && n < g.N) {
-      v = n < g.b.w1 ? ld4(g.b.p1 + long(k) * g.b.ld1 + n) : ld4(g.b.p2 + long(k) * g.b.ld2 + (n - g.b.w1));
+    if (k < K && c < width) {
+      v = c < src.w1 ? ld4(src.p1 + long(k) * src.ld1 + c) : ld4(src.p2 + long(k) * src.ld2 + (c - src.w1));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (n + j >= g.N) v[j] = 0.0f;
+        if (c + j >= width) v[j] = 0.0f;
     }
-    rb[i] = v;
+    r[i] = v;
   }
 }
 
-__device__ __forceinline__ void store_b(float* bs, int t, const f32x4 (&rb)[kLd]) {
+template <int C, int PITCH, int THREADS, int NLD>
+__device__ __forceinline__ void store_rows_lds(float* tile, int t, const f32x4 (&r)[NLD]) {
 #pragma unroll
-  for (int i = 0; i < kLd; ++i) {
-    const int idx = t + 256 * i;
-    *(f32x4*)(bs + (idx >> 5) * LDT + 4 * (idx & 31)) = rb[i];
+  for (int i = 0; i < NLD; ++i) {
+    const int idx = t + THREADS * i;
+    *(f32x4*)(tile + (idx / (C / 4)) * PITCH + 4 * (idx % (C / 4))) = r[i];
   }
 }
 
-// One LDS k tile into the wave's 64x64 accumulator block (2x2 MFMA tiles); with
-// kEpiPartial the first column tile also sums A over k for row t (the bias gradient).
-template <int kEpi>
-__device__ __forceinline__ void gemm_tile(const float* __restrict__ as, const float* __restrict__ bs,
-                                          f32x16 (&acc)[2][2], float& bsum, int wm, int wn, int h, int l32, int t) {
+// One LDS k tile into the wave's 64 x (32 TN) accumulator block; the first column
+// tile's threads t < BMT also add their row's BK dZ values to the bias sum.
+template <class T>
+__device__ __forceinline__ void wgrad_tile(const float* __restrict__ as, const float* __restrict__ bs,
+                                           f32x16 (&acc)[2][T::kTN], float& bsum, int wm, int wn, int h, int l32,
+                                           int t) {
 #pragma unroll
   for (int kk = 0; kk < BK / 2; ++kk) {
     const int k = 2 * kk + h;
-    const float a0 = as[k * LDT + wm * 64 + l32], a1 = as[k * LDT + wm * 64 + 32 + l32];
-    const float b0 = bs[k * LDT + wn * 64 + l32], b1 = bs[k * LDT + wn * 64 + 32 + l32];
-    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-  }
-  if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM) {
+    const float a0 = as[k * T::kPitchA + wm * 64 + l32], a1 = as[k * T::kPitchA + wm * 64 + 32 + l32];
+    float b[T::kTN];
 #pragma unroll
-    for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, as[kr * LDT + t]);
+    for (int j = 0; j < T::kTN; ++j) b[j] = bs[k * T::kPitchB + wn * 32 * T::kTN + 32 * j + l32];
+#pragma unroll
+    for (int j = 0; j < T::kTN; ++j) {
+      acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b[j], acc[0][j], 0, 0, 0);
+      acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b[j], acc[1][j], 0, 0, 0);
+    }
+  }
+  if (blockIdx.y == 0 && t < T::kWM * 64) {
+#pragma unroll
+    for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, as[kr * T::kPitchA + t]);
   }
 }
 
-template <bool kAK, int kEpi>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-  __shared__ float As[2][BK * LDT];
-  __shared__ float Bs[2][BK * LDT];
+template <int BMT, int BNT, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
+  using T = WTile<BMT, BNT, WAVES>;
+  __shared__ float As[2][BK * T::kPitchA];
+  __shared__ float Bs[2][BK * T::kPitchB];
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
-  const int wm = w & 1, wn = w >> 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  int kbeg = 0, kend = g.K;
-  if (kEpi == kEpiPartial) {
-    kbeg = blockIdx.z * g.k_split;
-    kend = min(g.K, kbeg + g.k_split);
-  }
+  const int wm = w % T::kWM, wn = w / T::kWM;
+  const int m0 = blockIdx.x * BMT, n0 = blockIdx.y * BNT;
+  const int kbeg = blockIdx.z * g.k_split;
+  const int kend = min(g.K, kbeg + g.k_split);
   const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  f32x16 acc[2][2];
+  f32x16 acc[2][T::kTN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < T::kTN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   float bsum = 0.0f;
-  auto load_tile = [&](int it, f32x4 (&ra)[kLd], f32x4 (&rb)[kLd]) {
-    load_a<kAK>(g, m0, kbeg + it * BK, t, ra);
-    load_b(g, n0, kbeg + it * BK, t, rb);
+  auto load_tile = [&](int it, f32x4 (&ra)[T::kLdA], f32x4 (&rb)[T::kLdB]) {
+    load_rows<BMT, T::kThreads, T::kLdA>(g.a, g.M, kend, m0, kbeg + it * BK, t, ra);
+    load_rows<BNT, T::kThreads, T::kLdB>(g.b, g.N, kend, n0, kbeg + it * BK, t, rb);
   };
-  auto store_tile = [&](int buf, const f32x4 (&ra)[kLd], const f32x4 (&rb)[kLd]) {
-    store_a<kAK>(As[buf], t, ra);
-    store_b(Bs[buf], t, rb);
+  auto store_tile = [&](int buf, const f32x4 (&ra)[T::kLdA], const f32x4 (&rb)[T::kLdB]) {
+    store_rows_lds<BMT, T::kPitchA, T::kThreads, T::kLdA>(As[buf], t, ra);
+    store_rows_lds<BNT, T::kPitchB, T::kThreads, T::kLdB>(Bs[buf], t, rb);
   };
   // k tiles staged two ahead: registers hold tile it+1 (landing) and tile it+2 (issued
   // this iteration) while LDS buffer it&1 is consumed; the register sets alternate by
-  // iteration parity, so the loop is unrolled by two
-  f32x4 ra0[kLd], rb0[kLd], ra1[kLd], rb1[kLd];
+  // iteration parity, so the loop is unrolled by two (-4.3 % step time against one ahead)
+  f32x4 ra0[T::kLdA], rb0[T::kLdB], ra1[T::kLdA], rb1[T::kLdB];
   if (nt > 0) {
     load_tile(0, ra0, rb0);
     store_tile(0, ra0, rb0);
@@ -263,34 +244,28 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   int it = 0;
   for (; it + 1 < nt; it += 2) {
     if (it + 2 < nt) load_tile(it + 2, ra0, rb0);
-    gemm_tile<kEpi>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);
+    wgrad_tile<T>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);
     store_tile(1, ra1, rb1);
     __syncthreads();
     if (it + 3 < nt) load_tile(it + 3, ra1, rb1);
-    gemm_tile<kEpi>(As[1], Bs[1], acc, bsum, wm, wn, h, l32, t);
+    wgrad_tile<T>(As[1], Bs[1], acc, bsum, wm, wn, h, l32, t);
     if (it + 2 < nt) store_tile(0, ra0, rb0);
     __syncthreads();
   }
-  if (it < nt) gemm_tile<kEpi>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);   // odd tile count: the last
-  float* c = g.c + (kEpi == kEpiPartial ? long(blockIdx.z) * g.c_split : 0L);
+  if (it < nt) wgrad_tile<T>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);   // odd tile count: the last
+  float* c = g.c + long(blockIdx.z) * g.c_split;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + l32;
-      const bool nok = n < g.N;
-      const int word = (n0 + wn * 64 + j * 32) >> 5;   // this 32-column group's word in a row
+    for (int j = 0; j < T::kTN; ++j) {
+      const int n = n0 + wn * 32 * T::kTN + 32 * j + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
-        const bool ok = nok && m < g.M;
-        float v = acc[i][j][r];
-        if (kEpi == kEpiMask && ok) v = (g.mask[long(m) * g.ldm + word] >> l32) & 1u ? v : 0.0f;
-        if (ok) c[long(m) * g.ldc + n] = v;
+        if (n < g.N && m < g.M) c[long(m) * g.ldc + n] = acc[i][j][r];
       }
     }
-  if (kEpi == kEpiPartial && blockIdx.y == 0 && t < BM && m0 + t < g.M)
-    g.bias_part[long(blockIdx.z) * g.M + m0 + t] = bsum;
+  if (blockIdx.y == 0 && t < BMT && m0 + t < g.M) g.bias_part[long(blockIdx.z) * g.M + m0 + t] = bsum;
 }
 
 // ---------------------------------------------------------- element-wise --
@@ -597,6 +572,113 @@ __global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restri
   }
 }
 
+// ------------------------------------------------ fused backward-data chain --
+// dZ_{l-1} = (W_l^T dZ_l) * bit(H_{l-1}) for the head and layers 7..1 in one launch, the
+// forward's register-stationary shape run backwards: dX^T[in, sample] = W^T[in, out] .
+// dZ^T[out, sample], so a layer's masked accumulator is the next one's B operand.  Starts
+// from the head's pre-activation gradient rows [P][132] (colour-0, density); writes dZ_l
+// rows [P][256] for l = 7..0 (the weight gradients' A operand), each stored piecewise
+// during the following layer as in the forward.
+template <int KU>
+__device__ __forceinline__ void bwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)[8], float dens,
+                                          const f32x4* __restrict__ blob, int lane, int h,
+                                          float* __restrict__ prev_row) {
+  constexpr int KH = KU == kHeadBwdKsteps ? kC0 / 2 : KU;   // k-steps fed by prev; the head's next is the density
+#pragma unroll
+  for (int o = 0; o < 8; ++o)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[o][r] = 0.0f;
+  const f32x4* a_base = blob + lane;
+#pragma unroll
+  for (int ug = 0; ug < KU / 4; ++ug) {
+    f32x4 a[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) a[o] = a_base[(ug * 8 + o) * 64];
+    if (prev_row != nullptr && ug < 32) {     // 256-wide dZ rows: 32 pieces of 16 B
+      const int t = ug >> 2, j = ug & 3;
+      *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
+          f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = 4 * ug + i;
+      const float b = u < KH ? prev[u >> 4][u & 15] : (u == KH && h == 0 ? dens : 0.0f);
+#pragma unroll
+      for (int o = 0; o < 8; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[o][i], b, acc[o], 0, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void apply_bits(f32x16 (&acc)[8], const u32x4_t (&w)[2], int h) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const unsigned word = w[t >> 2][t & 3];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = (word >> acc_row(r, h)) & 1u ? acc[t][r] : 0.0f;
+  }
+}
+
+struct BwdIo {
+  const float* dhc;          // [P][132]
+  const unsigned* mb[8];     // ReLU bits of H_0..H_7, [P][8]
+  float* dz[8];              // out: dZ_0..dZ_7 rows [P][256]
+};
+
+__global__ __launch_bounds__(256, 1) void train_bwd_kernel(const f32x4* __restrict__ blob, long n_points, BwdIo io) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const long p = (long(blockIdx.x) * 4 + wave) * kSamplesPerWave + (lane & 31);
+  const bool valid = p < n_points;
+  const long pc = valid ? p : n_points - 1;
+  f32x16 a[8], b[8];
+  // the head's gradient rows as a 4-tile "accumulator" (feature 32t + acc_row(r, h))
+  const float* row = io.dhc + pc * kHeadLd;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = ld4(row + 32 * t + 8 * j + 4 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[t][4 * j + q] = v[q];
+    }
+  const float dens = row[kC0];
+  u32x4_t w[2];
+  auto load_bits = [&](int l) {
+    const u32x4_t* src = (const u32x4_t*)(io.mb[l] + pc * (kH / 32));
+    w[0] = src[0];
+    w[1] = src[1];
+  };
+  float* const nul = nullptr;
+#define DZ(l) (valid ? io.dz[l] + p * kH : nul)
+  load_bits(7);
+  bwd_layer<kHeadBwdKsteps>(a, b, dens, blob + bwd_layer_offset(0) / 4, lane, h, nul);
+  apply_bits(a, w, h);                                              // dZ_7
+  load_bits(6);
+  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(1) / 4, lane, h, DZ(7));
+  apply_bits(b, w, h);                                              // dZ_6
+  load_bits(5);
+  bwd_layer<128>(a, b, 0.0f, blob + bwd_layer_offset(2) / 4, lane, h, DZ(6));
+  apply_bits(a, w, h);                                              // dZ_5
+  load_bits(4);
+  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(3) / 4, lane, h, DZ(5));
+  apply_bits(b, w, h);                                              // dZ_4
+  load_bits(3);
+  bwd_layer<128>(a, b, 0.0f, blob + bwd_layer_offset(4) / 4, lane, h, DZ(4));   // layer 4's hidden inputs
+  apply_bits(a, w, h);                                              // dZ_3
+  load_bits(2);
+  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(5) / 4, lane, h, DZ(3));
+  apply_bits(b, w, h);                                              // dZ_2
+  load_bits(1);
+  bwd_layer<128>(a, b, 0.0f, blob + bwd_layer_offset(6) / 4, lane, h, DZ(2));
+  apply_bits(a, w, h);                                              // dZ_1
+  load_bits(0);
+  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(7) / 4, lane, h, DZ(1));
+  apply_bits(b, w, h);                                              // dZ_0
+  if (valid) store_rows<8>(b, io.dz[0] + p * kH, h);
+#undef DZ
+}
+
 // --------------------------------------------------- gradient reduction --
 // Sums the split-K partials of one weight-gradient GEMM in split order and
 // scatters them into the flat gradients: rows [0, r1) to (w0 + m*ld0, n < nw0;
@@ -781,16 +863,7 @@ __global__ void relayout_kernel(const float* __restrict__ params, float* __restr
   const float* prm = params + blockIdx.y * kNetFloats;
   float* out = gemmw + blockIdx.y * kGemmFloats;
   float v = 0.0f;
-  if (e < kWcH) {
-    const long o = e - kW4h;
-    const int n = int(o / kH), k = int(o - long(n) * kH);
-    v = prm[w_off(4) + long(n) * kTrunkIn[4] + k];
-  } else if (e < kWcH + 144L * kH) {
-    const long o = e - kWcH;
-    const int n = int(o / kH), k = int(o - long(n) * kH);
-    if (n < kC0) v = prm[kFC0W + long(n) * kHeadK + k];
-    else if (n == kC0) v = prm[kFDensW + k];
-  } else if (e >= kF32Blob && e < kF32Blob + f32_blob_floats()) {
+  if (e < kF32Blob + f32_blob_floats()) {
     // pack.cpp's f32 blob, element by element: layer l, k-step group ug, tile o, lane, i
     long o = e - kF32Blob;
     int l = 0;
@@ -815,6 +888,19 @@ __global__ void relayout_kernel(const float* __restrict__ params, float* __restr
       v = prm[kFC1W + c * kC0 + 32 * t + acc_row(r, hh)];
     } else if (q >= kC1B && q < kC1B + 3) {
       v = prm[kFC1B + (q - kC1B)];
+    }
+  } else if (e >= kBwdBlob && e < kBwdBlob + bwd_layer_offset(kBwdLayers)) {
+    long o = e - kBwdBlob;
+    int b = 0;
+    while (b < kBwdLayers - 1 && o >= bwd_layer_floats(b)) o -= bwd_layer_floats(b++);
+    const int i4 = int(o & 3), lane = int((o >> 2) & 63), tile = int((o >> 8) & 7), ug = int(o >> 11);
+    const int u = 4 * ug + i4, hh = lane >> 5, in = 32 * tile + (lane & 31);
+    if (b == 0) {
+      if (u < kC0 / 2) v = prm[kFC0W + long(hid_f32_feature(u, hh)) * kHeadK + in];
+      else if (u == kC0 / 2 && hh == 0) v = prm[kFDensW + in];
+    } else {
+      const int l = bwd_trunk_layer(b);
+      v = prm[w_off(l) + long(hid_f32_feature(u, hh)) * kTrunkIn[l] + in];
     }
   }
   out[e] = v;
@@ -883,14 +969,14 @@ inline size_t al64(size_t x) { return (x + 63) / 64 * 64; }
 
 // Per-net activation arrays inside the workspace.
 struct Acts {
-  float *pe, *dpe, *h[8], *hc, *rgbs, *dpre, *tb, *dhc, *d0, *d1;
+  float *pe, *dpe, *h[8], *hc, *rgbs, *dpre, *tb, *dhc, *dz[8];
   unsigned* mb[8];   // ReLU bits of h[l]: [P][8] words
 };
 
 size_t acts_floats(long P) {
   const size_t p = size_t(P);
   return al64(p * kPeLd) + al64(p * kDpeLd) + 8 * al64(p * kH) + al64(p * kHeadLd) + 2 * al64(p * 4) + al64(p) +
-         al64(p * kHeadLd) + 2 * al64(p * kH) + 8 * al64(p * (kH / 32));
+         al64(p * kHeadLd) + 8 * al64(p * kH) + 8 * al64(p * (kH / 32));
 }
 
 size_t head_floats(int n_rays, int n_coarse) {
@@ -914,16 +1000,22 @@ Acts carve_acts(float* base, long P) {
   a.dpre = take(p * 4);
   a.tb = take(p);
   a.dhc = take(p * kHeadLd);
-  a.d0 = take(p * kH);
-  a.d1 = take(p * kH);
+  for (auto& d : a.dz) d = take(p * kH);
   for (auto& b : a.mb) b = (unsigned*)take(p * (kH / 32));
   return a;
 }
 
-template <bool kAK, int kEpi>
-hipError_t gemm(const GemmArgs& g, int splits, hipStream_t s) {
-  const dim3 grid{blocks_for(g.M, BM), blocks_for(g.N, BN), unsigned(kEpi == kEpiPartial ? splits : 1)};
-  hipLaunchKernelGGL((gemm_f32_kernel<kAK, kEpi>), grid, dim3(256), 0, s, g);
+// 256x256 tiles for M = N = 256, else 128x128
+bool big_tile(int M, int N) { return M == 256 && N == 256; }
+
+hipError_t launch_wgrad(const GemmArgs& g, int splits, hipStream_t s) {
+  if (big_tile(g.M, g.N)) {
+    const dim3 grid{blocks_for(g.M, 256), blocks_for(g.N, 256), unsigned(splits)};
+    hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 8>), grid, dim3(512), 0, s, g);
+  } else {
+    const dim3 grid{blocks_for(g.M, 128), blocks_for(g.N, 128), unsigned(splits)};
+    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 4>), grid, dim3(256), 0, s, g);
+  }
   return hipGetLastError();
 }
 
@@ -936,9 +1028,10 @@ struct WJob {
 
 WJob plan_wjob(int M, int N, long P, size_t& cursor) {
   WJob j{M, N, 1, 0, 0, 0};
-  const int tiles = int(blocks_for(M, BM) * blocks_for(N, BN));
+  const bool big = big_tile(M, N);
+  const int tiles = big ? int(blocks_for(M, 256) * blocks_for(N, 256)) : int(blocks_for(M, 128) * blocks_for(N, 128));
   const int ktiles = int(blocks_for(P, BK));
-  const int target = 2 * current_device_cus();
+  const int target = (big ? 1 : 2) * current_device_cus();   // 512-thread tiles: one workgroup per CU
   int splits = std::max(1, std::min(target / tiles, std::max(1, ktiles / 4)));
   j.k_split = int(blocks_for(ktiles, splits)) * BK;
   j.splits = int(blocks_for(P, j.k_split));
@@ -1021,7 +1114,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     g.bias_part = tr->part + j.boff;
     g.k_split = j.k_split;
     g.c_split = long(j.M) * j.N;
-    return gemm<false, kEpiPartial>(g, j.splits, s);
+    return launch_wgrad(g, j.splits, s);
   };
   hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jc1.splits), dim3(1024), 0, s, (const float*)a.dpre, 4, 3,
                      (const float*)a.hc, kHeadLd, kC0, P, kSkinnyChunk, tr->part + jc1.off, tr->part + jc1.boff);
@@ -1031,31 +1124,20 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   HIP_TRY(hipGetLastError());
   HIP_TRY(wgrad(jh, a.dhc, kHeadLd, Src2{a.h[7], a.dpe, kH, kDpeLd, kH}));
   {
-    GemmArgs g;   // d h7 = dhc . [colour-0 rows; density row] over the hidden inputs, ReLU mask of h7
-    g.M = int(P), g.N = kH, g.K = kHeadN;
-    g.a = Src2{a.dhc, nullptr, kHeadLd, 0, 0x7fffffff};
-    g.b = Src2{gw + kWcH, nullptr, kH, 0, 0x7fffffff};
-    g.c = a.d0, g.ldc = kH;
-    g.mask = a.mb[7], g.ldm = kH / 32;
-    HIP_TRY((gemm<true, kEpiMask>(g, 1, s)));
+    // dZ_7 .. dZ_0 in one launch (the head's and layers 7..1's data gradients with the ReLU bits)
+    BwdIo io;
+    io.dhc = a.dhc;
+    for (int l = 0; l < 8; ++l) io.mb[l] = a.mb[l], io.dz[l] = a.dz[l];
+    hipLaunchKernelGGL(train_bwd_kernel, dim3(blocks_for(P, 4 * kSamplesPerWave)), dim3(256), 0, s,
+                       (const f32x4*)(gw + kBwdBlob), P, io);
+    HIP_TRY(hipGetLastError());
   }
-  float* dz = a.d0;
-  float* dn = a.d1;
   for (int l = 7; l >= 0; --l) {
     Src2 X;
     if (l == 0) X = Src2{a.pe, nullptr, kPeLd, 0, 0x7fffffff};
     else if (l == 4) X = Src2{a.h[3], a.pe, kH, kPeLd, kH};
     else X = Src2{a.h[l - 1], nullptr, kH, 0, 0x7fffffff};
-    HIP_TRY(wgrad(jl[l], dz, kH, X));
-    if (l == 0) break;
-    GemmArgs g;
-    g.M = int(P), g.N = kH, g.K = kH;
-    g.a = Src2{dz, nullptr, kH, 0, 0x7fffffff};
-    g.b = l == 4 ? Src2{gw + kW4h, nullptr, kH, 0, 0x7fffffff} : Src2{prm + w_off(l), nullptr, kH, 0, 0x7fffffff};
-    g.c = dn, g.ldc = kH;
-    g.mask = a.mb[l - 1], g.ldm = kH / 32;
-    HIP_TRY((gemm<true, kEpiMask>(g, 1, s)));
-    std::swap(dz, dn);
+    HIP_TRY(wgrad(jl[l], a.dz[l], kH, X));
   }
   if ((rc = mark(4)) != NERF_OK) return rc;
 
