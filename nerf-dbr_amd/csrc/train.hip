@@ -113,10 +113,10 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------- weight gradients --
 // Partial weight gradients dW[m][n] = sum_k dZ[k][m] X[k][n] over one split of the samples
-// (k), on v_mfma_f32_32x32x2_f32: 256x256 tiles per 512-thread workgroup (8 waves x 64x128)
-// for the 256-wide layers, whose operands are then read once, 128x128 per 256 threads
-// (4 waves x 64x64) for the others; 16-deep k tiles double-buffered through LDS and
-// staged two ahead in registers.  Both operands are sample rows with the tile's 128 columns contiguous, so
+// (k), on v_mfma_f32_32x32x2_f32: one workgroup tile covers the whole [M][N] gradient
+// (256 x 256 over 8 waves of 64 x 128 for the 256-wide layers; launch_wgrad), so both
+// operands are read once; 16-deep k tiles double-buffered through LDS and staged two
+// ahead in registers.  Both operands are sample rows with the tile's 128 columns contiguous, so
 // every load is a float4 of a row and lands in LDS as is.  The first column tile also sums
 // dZ over k for its rows (the bias gradient).
 struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 % 4 == 0)
@@ -1005,17 +1005,20 @@ Acts carve_acts(float* base, long P) {
   return a;
 }
 
-// 256x256 tiles for M = N = 256, else 128x128
-bool big_tile(int M, int N) { return M == 256 && N == 256; }
+// One column tile spans all of N (128, 256 or 320 columns) and one row tile all of M, so
+// each operand row is read once, all over 8 waves: 256 x {128, 256, 320} (trunk layers 0
+// (63 columns), 1-3 / 5-7, 4 (319)), 128 x 384 (the colour-0 layer, 283).
+int tile_rows(int M) { return M >= 256 ? 256 : 128; }
+int tile_cols(int M, int N) { return N <= 128 ? 128 : N <= 256 ? 256 : tile_rows(M) == 256 ? 320 : 384; }
 
 hipError_t launch_wgrad(const GemmArgs& g, int splits, hipStream_t s) {
-  if (big_tile(g.M, g.N)) {
-    const dim3 grid{blocks_for(g.M, 256), blocks_for(g.N, 256), unsigned(splits)};
-    hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 8>), grid, dim3(512), 0, s, g);
-  } else {
-    const dim3 grid{blocks_for(g.M, 128), blocks_for(g.N, 128), unsigned(splits)};
-    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 4>), grid, dim3(256), 0, s, g);
-  }
+  const int bm = tile_rows(g.M), bn = tile_cols(g.M, g.N);
+  const dim3 grid{blocks_for(g.M, bm), blocks_for(g.N, bn), unsigned(splits)};
+  if (bm == 256 && bn == 256) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 8>), grid, dim3(512), 0, s, g);
+  else if (bm == 256 && bn == 320) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 320, 8>), grid, dim3(512), 0, s, g);
+  else if (bm == 256 && bn == 128) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 128, 8>), grid, dim3(512), 0, s, g);
+  else if (bm == 128 && bn == 384) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 384, 8>), grid, dim3(512), 0, s, g);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -1028,10 +1031,9 @@ struct WJob {
 
 WJob plan_wjob(int M, int N, long P, size_t& cursor) {
   WJob j{M, N, 1, 0, 0, 0};
-  const bool big = big_tile(M, N);
-  const int tiles = big ? int(blocks_for(M, 256) * blocks_for(N, 256)) : int(blocks_for(M, 128) * blocks_for(N, 128));
+  const int tiles = int(blocks_for(M, tile_rows(M)) * blocks_for(N, tile_cols(M, N)));
   const int ktiles = int(blocks_for(P, BK));
-  const int target = (big ? 1 : 2) * current_device_cus();   // 512-thread tiles: one workgroup per CU
+  const int target = current_device_cus();   // 8-wave tiles: one workgroup per CU
   int splits = std::max(1, std::min(target / tiles, std::max(1, ktiles / 4)));
   j.k_split = int(blocks_for(ktiles, splits)) * BK;
   j.splits = int(blocks_for(P, j.k_split));
