@@ -143,8 +143,8 @@ struct WTile {
   static constexpr int kThreads = 64 * WAVES;
   static constexpr int kWM = BMT / 64, kWN = WAVES / kWM;
   static constexpr int kTN = BNT / kWN / 32;                 // 32-column MFMA tiles per wave
-  static constexpr int kLdA = BK * BMT / 4 / kThreads;       // float4 per thread per k tile
-  static constexpr int kLdB = BK * BNT / 4 / kThreads;
+  static constexpr int kLdA = (BK * BMT / 4 + kThreads - 1) / kThreads;   // float4 per thread per k tile
+  static constexpr int kLdB = (BK * BNT / 4 + kThreads - 1) / kThreads;   // (the last may be partial)
   static constexpr int kPitchA = BMT + 4, kPitchB = BNT + 4; // LDS row pitches (floats)
   static_assert(kWM * kWN == WAVES && kTN >= 1 && kLdA >= 1 && kLdB >= 1, "tile geometry");
 };
@@ -159,7 +159,7 @@ __device__ __forceinline__ void load_rows(const Src2& src, int width, int K, int
     const int idx = t + THREADS * i;
     const int k = k0 + idx / (C / 4), c = c0 + 4 * (idx % (C / 4));
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (k < K && c < width) {
+    if (idx < BK * C / 4 && k < K && c < width) {
       v = c < src.w1 ? ld4(src.p1 + long(k) * src.ld1 + c) : ld4(src.p2 + long(k) * src.ld2 + (c - src.w1));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -174,7 +174,7 @@ __device__ __forceinline__ void store_rows_lds(float* tile, int t, const f32x4 (
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
     const int idx = t + THREADS * i;
-    *(f32x4*)(tile + (idx / (C / 4)) * PITCH + 4 * (idx % (C / 4))) = r[i];
+    if (idx < BK * C / 4) *(f32x4*)(tile + (idx / (C / 4)) * PITCH + 4 * (idx % (C / 4))) = r[i];
   }
 }
 
