@@ -149,32 +149,43 @@ struct WTile {
   static_assert(kWM * kWN == WAVES && kTN >= 1 && kLdA >= 1 && kLdB >= 1, "tile geometry");
 };
 
-// A thread's float4 pieces of a BK x C tile (columns c0.., rows k0..): sources hold at
-// least round_up4(width) valid floats per row; elements past the width or K are zero.
+// A thread's float4 pieces of the BK x C k tiles (columns c0.., rows k0..).  Every load
+// is issued unconditionally (so the compiler can count them: the LDS store of a k tile
+// waits only for that tile's loads, not for the next tile's, which stay in flight): a row
+// past K re-reads row K-1 and is zeroed when stored; a piece past the width reads column
+// 0 and feeds only output columns >= width, which are never stored, as do the columns of
+// a piece that straddles the width (sources hold round_up4(width) readable floats per row).
 template <int C, int THREADS, int NLD>
-__device__ __forceinline__ void load_rows(const Src2& src, int width, int K, int c0, int k0, int t,
-                                          f32x4 (&r)[NLD]) {
+struct RowPieces {
+  int off[NLD], row[NLD];     // column within the piece's source; row within the k tile
+  bool first[NLD];            // from the first source
+  __device__ __forceinline__ RowPieces(const Src2& src, int width, int c0, int t) {
 #pragma unroll
-  for (int i = 0; i < NLD; ++i) {
-    const int idx = t + THREADS * i;
-    const int k = k0 + idx / (C / 4), c = c0 + 4 * (idx % (C / 4));
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (idx < BK * C / 4 && k < K && c < width) {
-      v = c < src.w1 ? ld4(src.p1 + long(k) * src.ld1 + c) : ld4(src.p2 + long(k) * src.ld2 + (c - src.w1));
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (c + j >= width) v[j] = 0.0f;
+    for (int i = 0; i < NLD; ++i) {
+      const int idx = t + THREADS * i, c = c0 + 4 * (idx % (C / 4));
+      const bool ok = idx < BK * C / 4 && c < width;
+      row[i] = ok ? idx / (C / 4) : 0;
+      first[i] = !ok || c < src.w1;
+      off[i] = !ok ? 0 : first[i] ? c : c - src.w1;
     }
-    r[i] = v;
   }
-}
+  __device__ __forceinline__ void load(const Src2& src, int k0, int K, f32x4 (&r)[NLD]) const {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const long k = min(k0 + row[i], K - 1);
+      r[i] = first[i] ? ld4(src.p1 + (k * src.ld1 + off[i])) : ld4(src.p2 + (k * src.ld2 + off[i]));
+    }
+  }
+};
 
+// The k tile starting at k0 into LDS; rows past K as zeros.
 template <int C, int PITCH, int THREADS, int NLD>
-__device__ __forceinline__ void store_rows_lds(float* tile, int t, const f32x4 (&r)[NLD]) {
+__device__ __forceinline__ void store_rows_lds(float* tile, int t, int k0, int K, const f32x4 (&r)[NLD]) {
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
-    const int idx = t + THREADS * i;
-    if (idx < BK * C / 4) *(f32x4*)(tile + (idx / (C / 4)) * PITCH + 4 * (idx % (C / 4))) = r[i];
+    const int idx = t + THREADS * i, row = idx / (C / 4);
+    const f32x4 v = k0 + row < K ? r[i] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (idx < BK * C / 4) *(f32x4*)(tile + row * PITCH + 4 * (idx % (C / 4))) = v;
   }
 }
 
@@ -223,13 +234,15 @@ __global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   float bsum = 0.0f;
+  const RowPieces<BMT, T::kThreads, T::kLdA> pa(g.a, g.M, m0, t);
+  const RowPieces<BNT, T::kThreads, T::kLdB> pb(g.b, g.N, n0, t);
   auto load_tile = [&](int it, f32x4 (&ra)[T::kLdA], f32x4 (&rb)[T::kLdB]) {
-    load_rows<BMT, T::kThreads, T::kLdA>(g.a, g.M, kend, m0, kbeg + it * BK, t, ra);
-    load_rows<BNT, T::kThreads, T::kLdB>(g.b, g.N, kend, n0, kbeg + it * BK, t, rb);
+    pa.load(g.a, kbeg + it * BK, kend, ra);
+    pb.load(g.b, kbeg + it * BK, kend, rb);
   };
-  auto store_tile = [&](int buf, const f32x4 (&ra)[T::kLdA], const f32x4 (&rb)[T::kLdB]) {
-    store_rows_lds<BMT, T::kPitchA, T::kThreads, T::kLdA>(As[buf], t, ra);
-    store_rows_lds<BNT, T::kPitchB, T::kThreads, T::kLdB>(Bs[buf], t, rb);
+  auto store_tile = [&](int buf, int it, const f32x4 (&ra)[T::kLdA], const f32x4 (&rb)[T::kLdB]) {
+    store_rows_lds<BMT, T::kPitchA, T::kThreads, T::kLdA>(As[buf], t, kbeg + it * BK, kend, ra);
+    store_rows_lds<BNT, T::kPitchB, T::kThreads, T::kLdB>(Bs[buf], t, kbeg + it * BK, kend, rb);
   };
   // k tiles staged two ahead: registers hold tile it+1 (landing) and tile it+2 (issued
   // this iteration) while LDS buffer it&1 is consumed; the register sets alternate by
@@ -237,7 +250,7 @@ __global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
   f32x4 ra0[T::kLdA], rb0[T::kLdB], ra1[T::kLdA], rb1[T::kLdB];
   if (nt > 0) {
     load_tile(0, ra0, rb0);
-    store_tile(0, ra0, rb0);
+    store_tile(0, 0, ra0, rb0);
     if (nt > 1) load_tile(1, ra1, rb1);
     __syncthreads();
   }
@@ -245,11 +258,11 @@ __global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
   for (; it + 1 < nt; it += 2) {
     if (it + 2 < nt) load_tile(it + 2, ra0, rb0);
     wgrad_tile<T>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);
-    store_tile(1, ra1, rb1);
+    store_tile(1, it + 1, ra1, rb1);
     __syncthreads();
     if (it + 3 < nt) load_tile(it + 3, ra1, rb1);
     wgrad_tile<T>(As[1], Bs[1], acc, bsum, wm, wn, h, l32, t);
-    if (it + 2 < nt) store_tile(0, ra0, rb0);
+    if (it + 2 < nt) store_tile(0, it + 2, ra0, rb0);
     __syncthreads();
   }
   if (it < nt) wgrad_tile<T>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);   // odd tile count: the last
