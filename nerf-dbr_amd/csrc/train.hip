@@ -18,6 +18,7 @@
 #include <cstring>
 #include <vector>
 
+#include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
 
@@ -106,19 +107,21 @@ constexpr long kGemmFloats = kBwdBlob + round_up(int(bwd_layer_offset(kBwdLayers
 // Per-sample activation workspace (floats per sample; each array [P][ld])
 constexpr int kPeLd = 64, kDpeLd = 28;
 
-// 16-deep k tiles (32 with 128x128 tiles: two workgroups per CU instead of three, +11 %)
+// weight-gradient k tiles: 16 sample rows (one LDS-DMA buffer of 26-37 KiB, three in flight)
 constexpr int BK = 16;
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------- weight gradients --
 // Partial weight gradients dW[m][n] = sum_k dZ[k][m] X[k][n] over one split of the samples
-// (k), on v_mfma_f32_32x32x2_f32: one workgroup tile covers the whole [M][N] gradient
+// (k), on v_mfma_f32_32x32x2_f32.  One workgroup tile covers the whole [M][N] gradient
 // (256 x 256 over 8 waves of 64 x 128 for the 256-wide layers; launch_wgrad), so both
-// operands are read once; 16-deep k tiles double-buffered through LDS and staged two
-// ahead in registers.  Both operands are sample rows with the tile's 128 columns contiguous, so
-// every load is a float4 of a row and lands in LDS as is.  The first column tile also sums
-// dZ over k for its rows (the bias gradient).
+// operands are read once.  k tiles of BK sample rows move HBM -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: 1 KiB per wave instruction, no registers, no VALU), three
+// buffers deep and issued two tiles ahead: each wave waits for its own pieces with a
+// counted vmcnt, and one barrier per k tile publishes the tile and frees the buffer of the
+// tile before.  The first column tile's waves also sum dZ over k for their rows (the bias
+// gradient).
 struct Src2 {                // columns [0, w1) from p1, [w1, ...) from p2 (w1 % 4 == 0)
   const float* p1 = nullptr;
   const float* p2 = nullptr;
@@ -137,148 +140,155 @@ struct GemmArgs {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 
-// Workgroup tile BMT x BNT over WAVES waves, each wave 64 rows x (BNT / WN) columns.
-template <int BMT, int BNT, int WAVES>
-struct WTile {
+// Geometry of a k tile and of the workgroup tile.  LDS image of a k tile, each part
+// row-contiguous as in HBM: A [BK][BMT] (dZ rows), B1 [BK][W1] (the first source's
+// columns), B2 [BK][W2] (the second source's, e.g. layer 4's position encodings).  Every
+// wave issues the same number of DMA instructions per k tile (the list wraps around:
+// a repeated instruction writes the same bytes again), so one vmcnt count fits all.
+template <int BMT, int W1, int W2, int WAVES>
+struct WGeo {
   static constexpr int kThreads = 64 * WAVES;
   static constexpr int kWM = BMT / 64, kWN = WAVES / kWM;
-  static constexpr int kTN = BNT / kWN / 32;                 // 32-column MFMA tiles per wave
-  static constexpr int kLdA = (BK * BMT / 4 + kThreads - 1) / kThreads;   // float4 per thread per k tile
-  static constexpr int kLdB = (BK * BNT / 4 + kThreads - 1) / kThreads;   // (the last may be partial)
-  static constexpr int kPitchA = BMT + 4, kPitchB = BNT + 4; // LDS row pitches (floats)
-  static_assert(kWM * kWN == WAVES && kTN >= 1 && kLdA >= 1 && kLdB >= 1, "tile geometry");
+  // 32-column MFMA tiles of a wave (column group wn): kTN1 of B1 (columns 32 (kTN1 wn + j)),
+  // then B2's tiles b = wn, wn + kWN, ... (columns W1 + 32 b), so every tile lies in one
+  // part and its LDS rows have a constant stride
+  static constexpr int kTN1 = W1 / 32 / kWN, kTN2All = (W2 + 31) / 32;
+  static constexpr int kTN2 = (kTN2All + kWN - 1) / kWN;
+  static constexpr int kTN = kTN1 + kTN2;
+  static constexpr int kR16A = BMT / 4, kR16B1 = W1 / 4, kR16B2 = W2 / 4;   // 16-B pieces per row
+  static constexpr int kInsA = BK * kR16A / 64, kInsB1 = BK * kR16B1 / 64, kInsB2 = (BK * kR16B2 + 63) / 64;
+  static constexpr int kIns = kInsA + kInsB1 + kInsB2;
+  static constexpr int kInsPerWave = (kIns + WAVES - 1) / WAVES;
+  static constexpr int kOffB1 = BK * BMT * 4, kOffB2 = kOffB1 + BK * W1 * 4;
+  static constexpr int kBufBytes = round_up(kOffB2 + BK * W2 * 4 + 128, 1024);   // B2's last tile reads past W2
+  static constexpr int kBufs = 3;
+  static_assert(kWM * kWN == WAVES && kTN1 * 32 * kWN == W1, "tile geometry");
+  static_assert(BK * kR16A % 64 == 0 && BK * kR16B1 % 64 == 0, "whole DMA instructions");
+  static_assert(kBufs * kBufBytes <= 160 * 1024, "LDS budget");
 };
 
-// A thread's float4 pieces of the BK x C k tiles (columns c0.., rows k0..).  Every load
-// is issued unconditionally (so the compiler can count them: the LDS store of a k tile
-// waits only for that tile's loads, not for the next tile's, which stay in flight): a row
-// past K re-reads row K-1 and is zeroed when stored; a piece past the width reads column
-// 0 and feeds only output columns >= width, which are never stored, as do the columns of
-// a piece that straddles the width (sources hold round_up4(width) readable floats per row).
-template <int C, int THREADS, int NLD>
-struct RowPieces {
-  int off[NLD], row[NLD];     // column within the piece's source; row within the k tile
-  bool first[NLD];            // from the first source
-  __device__ __forceinline__ RowPieces(const Src2& src, int width, int c0, int t) {
+// The DMA instructions of this wave for the k tile at k0 into the buffer at LDS byte
+// address buf.  Rows past K re-read row K-1 (in bounds; A's are zeroed before use).
+template <int R16>
+__device__ __forceinline__ unsigned piece_off(int q, int lim, int ld) {   // R16 constant: no division
+  return unsigned(min(q / R16, lim) * ld * 4 + (q % R16) * 16);
+}
+template <class G>
+__device__ __forceinline__ void issue_ktile(const GemmArgs& g, int k0, int K, unsigned buf, int wave, int lane) {
+  const int lim = K - 1 - k0;
 #pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int idx = t + THREADS * i, c = c0 + 4 * (idx % (C / 4));
-      const bool ok = idx < BK * C / 4 && c < width;
-      row[i] = ok ? idx / (C / 4) : 0;
-      first[i] = !ok || c < src.w1;
-      off[i] = !ok ? 0 : first[i] ? c : c - src.w1;
+  for (int s = 0; s < G::kInsPerWave; ++s) {
+    const int ins = (s * (G::kThreads / 64) + wave) % G::kIns;   // wave-uniform
+    if (ins < G::kInsA) {
+      const int q = 64 * ins + lane;
+      lds_dma_16_s(g.a.p1 + long(k0) * g.a.ld1, piece_off<G::kR16A>(q, lim, g.a.ld1), buf + unsigned(ins * 1024));
+    } else if (ins < G::kInsA + G::kInsB1) {
+      const int ii = ins - G::kInsA, q = 64 * ii + lane;
+      lds_dma_16_s(g.b.p1 + long(k0) * g.b.ld1, piece_off<G::kR16B1>(q, lim, g.b.ld1),
+                   buf + unsigned(G::kOffB1 + ii * 1024));
+    } else if (G::kInsB2 > 0) {
+      const int ii = ins - G::kInsA - G::kInsB1, q = 64 * ii + lane;
+      if (q < BK * G::kR16B2)   // B2's last instruction may be partial
+        lds_dma_16_s(g.b.p2 + long(k0) * g.b.ld2, piece_off<(G::kR16B2 > 0 ? G::kR16B2 : 1)>(q, lim, g.b.ld2),
+                     buf + unsigned(G::kOffB2 + ii * 1024));
     }
-  }
-  __device__ __forceinline__ void load(const Src2& src, int k0, int K, f32x4 (&r)[NLD]) const {
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const long k = min(k0 + row[i], K - 1);
-      r[i] = first[i] ? ld4(src.p1 + (k * src.ld1 + off[i])) : ld4(src.p2 + (k * src.ld2 + off[i]));
-    }
-  }
-};
-
-// The k tile starting at k0 into LDS; rows past K as zeros.
-template <int C, int PITCH, int THREADS, int NLD>
-__device__ __forceinline__ void store_rows_lds(float* tile, int t, int k0, int K, const f32x4 (&r)[NLD]) {
-#pragma unroll
-  for (int i = 0; i < NLD; ++i) {
-    const int idx = t + THREADS * i, row = idx / (C / 4);
-    const f32x4 v = k0 + row < K ? r[i] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (idx < BK * C / 4) *(f32x4*)(tile + row * PITCH + 4 * (idx % (C / 4))) = v;
   }
 }
 
-// One LDS k tile into the wave's 64 x (32 TN) accumulator block; the first column
-// tile's threads t < BMT also add their row's BK dZ values to the bias sum.
-template <class T>
-__device__ __forceinline__ void wgrad_tile(const float* __restrict__ as, const float* __restrict__ bs,
-                                           f32x16 (&acc)[2][T::kTN], float& bsum, int wm, int wn, int h, int l32,
-                                           int t) {
+// Output column of the wave's column tile j (>= W1 + W2 when the wave has no such tile).
+template <class G, int W1>
+__device__ __forceinline__ int wtile_col(int wn, int j) {
+  return j < G::kTN1 ? 32 * (G::kTN1 * wn + j) : W1 + 32 * (wn + G::kWN * (j - G::kTN1));
+}
+
+// One k tile from LDS into the wave's 64 x (32 TN) accumulator block; waves of the first
+// column group also add their row's BK dZ values to the bias sum.
+template <class G, int BMT, int W1, int W2>
+__device__ __forceinline__ void wgrad_tile(const float* __restrict__ buf, f32x16 (&acc)[2][G::kTN], float& bsum,
+                                           int wm, int wn, int h, int l32, int t) {
+  const float* as = buf + wm * 64 + l32;
+  const float* b1 = buf + G::kOffB1 / 4 + 32 * G::kTN1 * wn + l32;
+  const float* b2 = buf + G::kOffB2 / 4 + 32 * wn + l32;
 #pragma unroll
   for (int kk = 0; kk < BK / 2; ++kk) {
     const int k = 2 * kk + h;
-    const float a0 = as[k * T::kPitchA + wm * 64 + l32], a1 = as[k * T::kPitchA + wm * 64 + 32 + l32];
-    float b[T::kTN];
+    const float a0 = as[k * BMT], a1 = as[k * BMT + 32];
+    float b[G::kTN];
 #pragma unroll
-    for (int j = 0; j < T::kTN; ++j) b[j] = bs[k * T::kPitchB + wn * 32 * T::kTN + 32 * j + l32];
+    for (int j = 0; j < G::kTN; ++j)
+      b[j] = j < G::kTN1 ? b1[k * W1 + 32 * j] : b2[k * W2 + 32 * G::kWN * (j - G::kTN1)];
 #pragma unroll
-    for (int j = 0; j < T::kTN; ++j) {
+    for (int j = 0; j < G::kTN; ++j) {
+      if (j >= G::kTN1 && wtile_col<G, W1>(wn, j) >= W1 + W2) continue;   // wave-uniform: no such tile
       acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b[j], acc[0][j], 0, 0, 0);
       acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b[j], acc[1][j], 0, 0, 0);
     }
   }
-  if (blockIdx.y == 0 && t < T::kWM * 64) {
+  if (t < BMT) {
 #pragma unroll
-    for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, as[kr * T::kPitchA + t]);
+    for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, buf[kr * BMT + t]);
   }
 }
 
-template <int BMT, int BNT, int WAVES>
+template <int BMT, int W1, int W2, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
-  using T = WTile<BMT, BNT, WAVES>;
-  __shared__ float As[2][BK * T::kPitchA];
-  __shared__ float Bs[2][BK * T::kPitchB];
+  using G = WGeo<BMT, W1, W2, WAVES>;
+  __shared__ __attribute__((aligned(1024))) float lds[G::kBufs * G::kBufBytes / 4];
   const int t = threadIdx.x;
-  const int lane = t & 63, w = t >> 6, h = lane >> 5, l32 = lane & 31;
-  const int wm = w % T::kWM, wn = w / T::kWM;
-  const int m0 = blockIdx.x * BMT, n0 = blockIdx.y * BNT;
+  const int lane = t & 63, h = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w % G::kWM, wn = w / G::kWM;
   const int kbeg = blockIdx.z * g.k_split;
   const int kend = min(g.K, kbeg + g.k_split);
   const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  f32x16 acc[2][T::kTN];
+  const unsigned lds0 = lds_addr(lds);
+  f32x16 acc[2][G::kTN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < T::kTN; ++j)
+    for (int j = 0; j < G::kTN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   float bsum = 0.0f;
-  const RowPieces<BMT, T::kThreads, T::kLdA> pa(g.a, g.M, m0, t);
-  const RowPieces<BNT, T::kThreads, T::kLdB> pb(g.b, g.N, n0, t);
-  auto load_tile = [&](int it, f32x4 (&ra)[T::kLdA], f32x4 (&rb)[T::kLdB]) {
-    pa.load(g.a, kbeg + it * BK, kend, ra);
-    pb.load(g.b, kbeg + it * BK, kend, rb);
-  };
-  auto store_tile = [&](int buf, int it, const f32x4 (&ra)[T::kLdA], const f32x4 (&rb)[T::kLdB]) {
-    store_rows_lds<BMT, T::kPitchA, T::kThreads, T::kLdA>(As[buf], t, kbeg + it * BK, kend, ra);
-    store_rows_lds<BNT, T::kPitchB, T::kThreads, T::kLdB>(Bs[buf], t, kbeg + it * BK, kend, rb);
-  };
-  // k tiles staged two ahead: registers hold tile it+1 (landing) and tile it+2 (issued
-  // this iteration) while LDS buffer it&1 is consumed; the register sets alternate by
-  // iteration parity, so the loop is unrolled by two (-4.3 % step time against one ahead)
-  f32x4 ra0[T::kLdA], rb0[T::kLdB], ra1[T::kLdA], rb1[T::kLdB];
-  if (nt > 0) {
-    load_tile(0, ra0, rb0);
-    store_tile(0, 0, ra0, rb0);
-    if (nt > 1) load_tile(1, ra1, rb1);
-    __syncthreads();
+  // tiles 0 and 1 in flight; iteration it: own pieces of tile it landed (tile it+1's
+  // may still be in flight), barrier (tile it published, buffer of tile it-1 free),
+  // tile it+2 into that buffer, then tile it from LDS
+  if (nt > 0) issue_ktile<G>(g, kbeg, kend, lds0, w, lane);
+  if (nt > 1) issue_ktile<G>(g, kbeg + BK, kend, lds0 + G::kBufBytes, w, lane);
+  int buf = 0;
+  for (int it = 0; it < nt; ++it) {
+    if (it + 1 < nt) wait_vmcnt(G::kInsPerWave);
+    else wait_vmcnt(0);
+    compiler_fence();
+    __builtin_amdgcn_s_barrier();
+    compiler_fence();
+    if (it + 2 < nt) {
+      const int b2 = buf >= 1 ? buf - 1 : G::kBufs - 1;      // (it + 2) % 3
+      issue_ktile<G>(g, kbeg + (it + 2) * BK, kend, lds0 + unsigned(b2 * G::kBufBytes), w, lane);
+    }
+    float* cur = lds + buf * (G::kBufBytes / 4);
+    const int valid = kend - (kbeg + it * BK);
+    if (valid < BK) {                 // the split's partial last k tile: A rows past K as zeros
+      for (int i = t; i < BK * BMT; i += G::kThreads)
+        if (i / BMT >= valid) cur[i] = 0.0f;
+      __syncthreads();
+    }
+    wgrad_tile<G, BMT, W1, W2>(cur, acc, bsum, wm, wn, h, l32, t);
+    buf = buf + 1 == G::kBufs ? 0 : buf + 1;
   }
-  int it = 0;
-  for (; it + 1 < nt; it += 2) {
-    if (it + 2 < nt) load_tile(it + 2, ra0, rb0);
-    wgrad_tile<T>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);
-    store_tile(1, it + 1, ra1, rb1);
-    __syncthreads();
-    if (it + 3 < nt) load_tile(it + 3, ra1, rb1);
-    wgrad_tile<T>(As[1], Bs[1], acc, bsum, wm, wn, h, l32, t);
-    if (it + 2 < nt) store_tile(0, it + 2, ra0, rb0);
-    __syncthreads();
-  }
-  if (it < nt) wgrad_tile<T>(As[0], Bs[0], acc, bsum, wm, wn, h, l32, t);   // odd tile count: the last
   float* c = g.c + long(blockIdx.z) * g.c_split;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < T::kTN; ++j) {
-      const int n = n0 + wn * 32 * T::kTN + 32 * j + l32;
+    for (int j = 0; j < G::kTN; ++j) {
+      const int n = wtile_col<G, W1>(wn, j) + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
+        const int m = wm * 64 + i * 32 + acc_row(r, h);
         if (n < g.N && m < g.M) c[long(m) * g.ldc + n] = acc[i][j][r];
       }
     }
-  if (blockIdx.y == 0 && t < BMT && m0 + t < g.M) g.bias_part[long(blockIdx.z) * g.M + m0 + t] = bsum;
+  if (t < BMT && t < g.M) g.bias_part[long(blockIdx.z) * g.M + t] = bsum;
 }
 
 // ---------------------------------------------------------- element-wise --
@@ -1021,21 +1031,26 @@ Acts carve_acts(float* base, long P) {
 // One column tile spans all of N (128, 256 or 320 columns) and one row tile all of M, so
 // each operand row is read once, all over 8 waves: 256 x {128, 256, 320} (trunk layers 0
 // (63 columns), 1-3 / 5-7, 4 (319)), 128 x 384 (the colour-0 layer, 283).
-int tile_rows(int M) { return M >= 256 ? 256 : 128; }
-int tile_cols(int M, int N) { return N <= 128 ? 128 : N <= 256 ? 256 : tile_rows(M) == 256 ? 320 : 384; }
-
+// The four weight-gradient shapes of a NeRFModel (M x N: B's sources)
+//   256 x 256: the previous layer's rows; 256 x 319: [layer 3's rows, the position
+//   encodings]; 256 x 63: the position encodings; 128 x 283: [layer 7's rows, the direction
+//   encodings].  Each runs as one workgroup tile; the host checks the operands fit it.
 hipError_t launch_wgrad(const GemmArgs& g, int splits, hipStream_t s) {
-  const int bm = tile_rows(g.M), bn = tile_cols(g.M, g.N);
-  const dim3 grid{blocks_for(g.M, bm), blocks_for(g.N, bn), unsigned(splits)};
-  if (bm == 256 && bn == 256) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 8>), grid, dim3(512), 0, s, g);
-  else if (bm == 256 && bn == 320) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 320, 8>), grid, dim3(512), 0, s, g);
-  else if (bm == 256 && bn == 128) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 128, 8>), grid, dim3(512), 0, s, g);
-  else if (bm == 128 && bn == 384) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 384, 8>), grid, dim3(512), 0, s, g);
+  const bool two = g.b.w1 < g.N;
+  const int W1 = two ? g.b.w1 : round_up(g.N, 4), W2 = two ? round_up(g.N - g.b.w1, 4) : 0;
+  auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (g.a.ld1 % 4 || g.b.ld1 % 4 || (two && (g.b.ld2 % 4 || W2 > g.b.ld2)) || W1 > g.b.ld1 || g.M > g.a.ld1 ||
+      !aligned(g.a.p1) || !aligned(g.b.p1) || (two && !aligned(g.b.p2)))
+    return hipErrorInvalidValue;
+  const dim3 grid{1, 1, unsigned(splits)};
+  if (g.M == 256 && W1 == 256 && W2 == 0) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 0, 8>), grid, dim3(512), 0, s, g);
+  else if (g.M == 256 && W1 == 256 && W2 == 64) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 64, 8>), grid, dim3(512), 0, s, g);
+  else if (g.M == 256 && W1 == 64 && W2 == 0) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 64, 0, 8>), grid, dim3(512), 0, s, g);
+  else if (g.M == 128 && W1 == 256 && W2 == 28) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 256, 28, 8>), grid, dim3(512), 0, s, g);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-// Weight-gradient GEMM job: k split over the samples so that the grid fills the chip.
 struct WJob {
   int M, N;
   int splits, k_split;
@@ -1044,7 +1059,7 @@ struct WJob {
 
 WJob plan_wjob(int M, int N, long P, size_t& cursor) {
   WJob j{M, N, 1, 0, 0, 0};
-  const int tiles = int(blocks_for(M, tile_rows(M)) * blocks_for(N, tile_cols(M, N)));
+  const int tiles = 1;                       // one workgroup tile per job (launch_wgrad)
   const int ktiles = int(blocks_for(P, BK));
   const int target = current_device_cus();   // 8-wave tiles: one workgroup per CU
   int splits = std::max(1, std::min(target / tiles, std::max(1, ktiles / 4)));
