@@ -14,6 +14,7 @@
 //   run backwards (dZ of every layer written) -> weight gradients as split-K GEMM partials
 //   over the samples -> one reduction into the flat gradients -> grad norm, clip, Adam,
 //   and the relayout of the updated weights into the two kernels' fragment blobs.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -115,7 +116,7 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 // ------------------------------------------------------- weight gradients --
 // Partial weight gradients dW[m][n] = sum_k dZ[k][m] X[k][n] over one split of the samples
 // (k), on v_mfma_f32_32x32x2_f32.  One workgroup tile covers the whole [M][N] gradient
-// (256 x 256 over 8 waves of 64 x 128 for the 256-wide layers; launch_wgrad), so both
+// (256 x 256 over 8 waves of 64 x 128 for the 256-wide layers; wgrad_shape), so both
 // operands are read once.  k tiles of BK sample rows move HBM -> LDS by LDS-DMA
 // (global_load_lds_dwordx4: 1 KiB per wave instruction, no registers, no VALU), three
 // buffers deep and issued two tiles ahead: each wave waits for its own pieces with a
@@ -230,15 +231,27 @@ __device__ __forceinline__ void wgrad_tile(const float* __restrict__ buf, f32x16
   }
 }
 
+// One split (k range) of one job: the workgroup's whole M x N partial.
+// An opaque SGPR copy: the job's arguments come from a dynamically indexed kernel-argument
+// table, and without this the compiler re-loads them per use inside the k loop (each
+// reload's lgkmcnt(0) also waits for every LDS read in flight).
+template <typename T>
+__device__ __forceinline__ T pin_sgpr(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
 template <int BMT, int W1, int W2, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void wgrad_split(GemmArgs g, int split, float* lds) {
   using G = WGeo<BMT, W1, W2, WAVES>;
-  __shared__ __attribute__((aligned(1024))) float lds[G::kBufs * G::kBufBytes / 4];
+  g.a.p1 = pin_sgpr(g.a.p1), g.b.p1 = pin_sgpr(g.b.p1), g.b.p2 = pin_sgpr(g.b.p2);
+  g.a.ld1 = pin_sgpr(g.a.ld1), g.b.ld1 = pin_sgpr(g.b.ld1), g.b.ld2 = pin_sgpr(g.b.ld2);
+  g.K = pin_sgpr(g.K), g.k_split = pin_sgpr(g.k_split);
   const int t = threadIdx.x;
   const int lane = t & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w % G::kWM, wn = w / G::kWM;
-  const int kbeg = blockIdx.z * g.k_split;
+  const int kbeg = split * g.k_split;
   const int kend = min(g.K, kbeg + g.k_split);
   const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const unsigned lds0 = lds_addr(lds);
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
     wgrad_tile<G, BMT, W1, W2>(cur, acc, bsum, wm, wn, h, l32, t);
     buf = buf + 1 == G::kBufs ? 0 : buf + 1;
   }
-  float* c = g.c + long(blockIdx.z) * g.c_split;
+  float* c = g.c + long(split) * g.c_split;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -288,7 +301,38 @@ __global__ __launch_bounds__(64 * WAVES) void wgrad_gemm_kernel(GemmArgs g) {
         if (n < g.N && m < g.M) c[long(m) * g.ldc + n] = acc[i][j][r];
       }
     }
-  if (t < BMT && t < g.M) g.bias_part[long(blockIdx.z) * g.M + t] = bsum;
+  if (t < BMT && t < g.M) g.bias_part[long(split) * g.M + t] = bsum;
+}
+
+// All weight-gradient jobs of a net in one launch (they only need the forward's rows and
+// the backward-data chain's dZ): job j owns workgroups [first[j], first[j+1]), one split
+// each, with splits in proportion to the job's MFMA work, so every CU gets about the same
+// work, the chip fills once, and the partials (one M x N block per workgroup) stay few.
+enum WShape { kW256x256 = 0, kW256x319, kW256x63, kW128x283, kNumWShapes };
+constexpr int kMaxWJobs = 9;
+struct WGroup {
+  GemmArgs g[kMaxWJobs];
+  int shape[kMaxWJobs];
+  int first[kMaxWJobs + 1];
+  int n;
+};
+constexpr int kWgradLdsBytes = std::max(
+    std::max(WGeo<256, 256, 0, 8>::kBufs * WGeo<256, 256, 0, 8>::kBufBytes,
+             WGeo<256, 256, 64, 8>::kBufs * WGeo<256, 256, 64, 8>::kBufBytes),
+    std::max(WGeo<256, 64, 0, 8>::kBufs * WGeo<256, 64, 0, 8>::kBufBytes,
+             WGeo<128, 256, 28, 8>::kBufs * WGeo<128, 256, 28, 8>::kBufBytes));
+
+__global__ __launch_bounds__(512) void wgrad_group_kernel(WGroup grp) {
+  __shared__ __attribute__((aligned(1024))) float lds[kWgradLdsBytes / 4];
+  int j = 0;
+  while (j + 1 < grp.n && int(blockIdx.x) >= grp.first[j + 1]) ++j;
+  const int split = int(blockIdx.x) - grp.first[j];
+  switch (grp.shape[j]) {
+    case kW256x256: wgrad_split<256, 256, 0, 8>(grp.g[j], split, lds); break;
+    case kW256x319: wgrad_split<256, 256, 64, 8>(grp.g[j], split, lds); break;
+    case kW256x63: wgrad_split<256, 64, 0, 8>(grp.g[j], split, lds); break;
+    default: wgrad_split<128, 256, 28, 8>(grp.g[j], split, lds); break;
+  }
 }
 
 // ---------------------------------------------------------- element-wise --
@@ -753,6 +797,37 @@ __global__ void reduce_grads_kernel(RedJobs jobs, float* __restrict__ grads) {
   grads[dst] = __fadd_rn(__fadd_rn(s4[0], s4[1]), __fadd_rn(s4[2], s4[3]));
 }
 
+// The same reduction for jobs with many splits (the skinny layers': one per 256 samples):
+// one workgroup per element, thread t sums splits t, t + 256, ..., then a fixed-order tree
+// over the 256 threads (deterministic).
+__global__ __launch_bounds__(256) void reduce_wide_kernel(RedJobs jobs, int first, float* __restrict__ grads) {
+  const RedJob& jb = jobs.j[first + blockIdx.y];
+  const long e = blockIdx.x;
+  const long mn = long(jb.M) * jb.N;
+  if (e >= mn + jb.M) return;                            // uniform per workgroup
+  const float* src;
+  long stride, dst;
+  if (e < mn) {
+    const int m = int(e / jb.N), n = int(e - long(m) * jb.N);
+    src = jb.part + e, stride = mn;
+    dst = jb.w0 + long(m) * jb.ld0 + n;
+  } else {
+    const int m = int(e - mn);
+    src = jb.bpart + m, stride = jb.M;
+    dst = jb.b0 + m;
+  }
+  __shared__ float red[256];
+  float acc = 0.0f;
+  for (int k = threadIdx.x; k < jb.splits; k += 256) acc = __fadd_rn(acc, src[k * stride]);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (int(threadIdx.x) < w) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) grads[dst] = red[0];
+}
+
 // Weight gradients of the skinny layers (colour-1: 3 rows over the 128 colour-0 outputs;
 // density: 1 row over the 256 trunk outputs): partial[split][m][n] = sum over the
 // split's samples of A[p][m] * B[p][n], and the bias partials sum_p A[p][m].
@@ -1035,20 +1110,18 @@ Acts carve_acts(float* base, long P) {
 //   256 x 256: the previous layer's rows; 256 x 319: [layer 3's rows, the position
 //   encodings]; 256 x 63: the position encodings; 128 x 283: [layer 7's rows, the direction
 //   encodings].  Each runs as one workgroup tile; the host checks the operands fit it.
-hipError_t launch_wgrad(const GemmArgs& g, int splits, hipStream_t s) {
+int wgrad_shape(const GemmArgs& g) {
   const bool two = g.b.w1 < g.N;
   const int W1 = two ? g.b.w1 : round_up(g.N, 4), W2 = two ? round_up(g.N - g.b.w1, 4) : 0;
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (g.a.ld1 % 4 || g.b.ld1 % 4 || (two && (g.b.ld2 % 4 || W2 > g.b.ld2)) || W1 > g.b.ld1 || g.M > g.a.ld1 ||
       !aligned(g.a.p1) || !aligned(g.b.p1) || (two && !aligned(g.b.p2)))
-    return hipErrorInvalidValue;
-  const dim3 grid{1, 1, unsigned(splits)};
-  if (g.M == 256 && W1 == 256 && W2 == 0) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 0, 8>), grid, dim3(512), 0, s, g);
-  else if (g.M == 256 && W1 == 256 && W2 == 64) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 256, 64, 8>), grid, dim3(512), 0, s, g);
-  else if (g.M == 256 && W1 == 64 && W2 == 0) hipLaunchKernelGGL((wgrad_gemm_kernel<256, 64, 0, 8>), grid, dim3(512), 0, s, g);
-  else if (g.M == 128 && W1 == 256 && W2 == 28) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 256, 28, 8>), grid, dim3(512), 0, s, g);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+    return -1;
+  if (g.M == 256 && W1 == 256 && W2 == 0) return kW256x256;
+  if (g.M == 256 && W1 == 256 && W2 == 64) return kW256x319;
+  if (g.M == 256 && W1 == 64 && W2 == 0) return kW256x63;
+  if (g.M == 128 && W1 == 256 && W2 == 28) return kW128x283;
+  return -1;
 }
 
 struct WJob {
@@ -1057,12 +1130,10 @@ struct WJob {
   size_t off, boff;   // partial and bias-partial offsets in the part buffer
 };
 
-WJob plan_wjob(int M, int N, long P, size_t& cursor) {
+WJob plan_wjob(int M, int N, long P, int want, size_t& cursor) {
   WJob j{M, N, 1, 0, 0, 0};
-  const int tiles = 1;                       // one workgroup tile per job (launch_wgrad)
   const int ktiles = int(blocks_for(P, BK));
-  const int target = current_device_cus();   // 8-wave tiles: one workgroup per CU
-  int splits = std::max(1, std::min(target / tiles, std::max(1, ktiles / 4)));
+  const int splits = std::max(1, std::min(want, std::max(1, ktiles / 4)));
   j.k_split = int(blocks_for(ktiles, splits)) * BK;
   j.splits = int(blocks_for(P, j.k_split));
   j.off = cursor;
@@ -1070,6 +1141,31 @@ WJob plan_wjob(int M, int N, long P, size_t& cursor) {
   j.boff = cursor;
   cursor += al64(size_t(j.splits) * M);
   return j;
+}
+
+// Workgroups per weight-gradient job of a net, one per CU in all: in proportion to the
+// job's time per sample, measured on MI355X with each job alone on the chip (rocprofv3,
+// main.py's config; relative to a 256 x 256 layer): 256 x 319 1.30, 256 x 63 0.34,
+// 128 x 283 0.74 (its column tiles do not split evenly over the SIMDs).
+void wgrad_splits(int (&want)[kMaxWJobs]) {
+  double w[kMaxWJobs], total = 0.0;
+  for (int l = 0; l < 8; ++l) w[l] = l == 0 ? 0.34 : l == 4 ? 1.30 : 1.0;
+  w[8] = 0.74;
+  for (double x : w) total += x;
+  const int cus = current_device_cus();
+  int sum = 0;
+  double frac[kMaxWJobs];
+  for (int i = 0; i < kMaxWJobs; ++i) {
+    const double e = cus * w[i] / total;
+    sum += (want[i] = std::max(1, int(e)));
+    frac[i] = e - int(e);
+  }
+  while (sum < cus) {                     // leftover CUs to the largest remainders
+    int b = 0;
+    for (int i = 1; i < kMaxWJobs; ++i)
+      if (frac[i] > frac[b]) b = i;
+    ++want[b], ++sum, frac[b] = -1.0;
+  }
 }
 
 double gemm_macs_per_sample() {
@@ -1131,28 +1227,18 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     j->boff = cur;
     cur += al64(size_t(j->splits) * j->M);
   }
-  WJob jh = plan_wjob(kC0, kHeadK, P, cur);
+  int want[kMaxWJobs];
+  wgrad_splits(want);
   WJob jl[8];
-  for (int l = 7; l >= 0; --l) jl[l] = plan_wjob(kH, kTrunkIn[l], P, cur);
+  for (int l = 7; l >= 0; --l) jl[l] = plan_wjob(kH, kTrunkIn[l], P, want[l], cur);
+  WJob jh = plan_wjob(kC0, kHeadK, P, want[8], cur);
   if ((rc = grow_buf(tr->part, tr->part_cap, cur, "gradient partials")) != NERF_OK) return rc;
-  auto wgrad = [&](const WJob& j, const float* A, int lda, Src2 B) -> hipError_t {
-    GemmArgs g;
-    g.M = j.M, g.N = j.N, g.K = int(P);
-    g.a = Src2{A, nullptr, lda, 0, 0x7fffffff};
-    g.b = B;
-    g.c = tr->part + j.off, g.ldc = j.N;
-    g.bias_part = tr->part + j.boff;
-    g.k_split = j.k_split;
-    g.c_split = long(j.M) * j.N;
-    return launch_wgrad(g, j.splits, s);
-  };
   hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jc1.splits), dim3(1024), 0, s, (const float*)a.dpre, 4, 3,
                      (const float*)a.hc, kHeadLd, kC0, P, kSkinnyChunk, tr->part + jc1.off, tr->part + jc1.boff);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jd.splits), dim3(1024), 0, s, (const float*)a.dpre + 3, 4, 1,
                      (const float*)a.h[7], kH, kH, P, kSkinnyChunk, tr->part + jd.off, tr->part + jd.boff);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(wgrad(jh, a.dhc, kHeadLd, Src2{a.h[7], a.dpe, kH, kDpeLd, kH}));
   {
     // dZ_7 .. dZ_0 in one launch (the head's and layers 7..1's data gradients with the ReLU bits)
     BwdIo io;
@@ -1162,12 +1248,36 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
                        (const f32x4*)(gw + kBwdBlob), P, io);
     HIP_TRY(hipGetLastError());
   }
-  for (int l = 7; l >= 0; --l) {
-    Src2 X;
-    if (l == 0) X = Src2{a.pe, nullptr, kPeLd, 0, 0x7fffffff};
-    else if (l == 4) X = Src2{a.h[3], a.pe, kH, kPeLd, kH};
-    else X = Src2{a.h[l - 1], nullptr, kH, 0, 0x7fffffff};
-    HIP_TRY(wgrad(jl[l], a.dz[l], kH, X));
+  {
+    // every weight-gradient GEMM of the net in one launch
+    WGroup grp{};
+    int nwg = 0;
+    auto add = [&](const WJob& j, const float* A, int lda, Src2 B) -> bool {
+      GemmArgs& g = grp.g[grp.n];
+      g.M = j.M, g.N = j.N, g.K = int(P);
+      g.a = Src2{A, nullptr, lda, 0, 0x7fffffff};
+      g.b = B;
+      g.c = tr->part + j.off, g.ldc = j.N;
+      g.bias_part = tr->part + j.boff;
+      g.k_split = j.k_split;
+      g.c_split = long(j.M) * j.N;
+      if ((grp.shape[grp.n] = wgrad_shape(g)) < 0) return false;
+      grp.first[grp.n++] = nwg;
+      nwg += j.splits;
+      return true;
+    };
+    bool ok = add(jh, a.dhc, kHeadLd, Src2{a.h[7], a.dpe, kH, kDpeLd, kH});
+    for (int l = 7; l >= 0; --l) {
+      Src2 X;
+      if (l == 0) X = Src2{a.pe, nullptr, kPeLd, 0, 0x7fffffff};
+      else if (l == 4) X = Src2{a.h[3], a.pe, kH, kPeLd, kH};
+      else X = Src2{a.h[l - 1], nullptr, kH, 0, 0x7fffffff};
+      ok = ok && add(jl[l], a.dz[l], kH, X);
+    }
+    if (!ok) return set_error(NERF_E_INVALID, "weight-gradient operands do not fit a kernel shape");
+    grp.first[grp.n] = nwg;
+    hipLaunchKernelGGL(wgrad_group_kernel, dim3(nwg), dim3(512), 0, s, grp);
+    HIP_TRY(hipGetLastError());
   }
   if ((rc = mark(4)) != NERF_OK) return rc;
 
@@ -1186,7 +1296,11 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   job(9, jd, 1, kFDensW, kFDensB, kH, kH, 0, 0, 0, 0);
   job(10, jc1, 3, kFC1W, kFC1B, kC0, kC0, 0, 0, 0, 0);
   maxe = std::max(maxe, long(jh.M) * jh.N + jh.M);
-  hipLaunchKernelGGL(reduce_grads_kernel, dim3(blocks_for(maxe, 256), 11), dim3(256), 0, s, jobs, grads);
+  hipLaunchKernelGGL(reduce_grads_kernel, dim3(blocks_for(maxe, 256), 9), dim3(256), 0, s, jobs, grads);
+  HIP_TRY(hipGetLastError());
+  // the skinny layers' partials (one split per 256 samples): a workgroup per element
+  hipLaunchKernelGGL(reduce_wide_kernel, dim3(std::max(long(jd.M) * jd.N + jd.M, long(jc1.M) * jc1.N + jc1.M), 2),
+                     dim3(256), 0, s, jobs, 9, grads);
   HIP_TRY(hipGetLastError());
   tr->gemm_flops += 2.0 * gemm_macs_per_sample() * double(P);
   return NERF_OK;
