@@ -828,49 +828,64 @@ __global__ __launch_bounds__(256) void reduce_wide_kernel(RedJobs jobs, int firs
   if (threadIdx.x == 0) grads[dst] = red[0];
 }
 
-// Weight gradients of the skinny layers (colour-1: 3 rows over the 128 colour-0 outputs;
-// density: 1 row over the 256 trunk outputs): partial[split][m][n] = sum over the
-// split's samples of A[p][m] * B[p][n], and the bias partials sum_p A[p][m].
-// 1024 threads: column n = t % 256, sample phase t / 256 (every 4th sample of the
-// split); the four phase sums are then added in a fixed order.  B rows are read whole.
-__global__ __launch_bounds__(1024) void skinny_wgrad_kernel(const float* __restrict__ A, int lda, int M,
-                                                            const float* __restrict__ B, int ldb, int N, long P,
-                                                            int chunk, float* __restrict__ part,
-                                                            float* __restrict__ bpart) {
-  __shared__ float red[4][4][256];
+// Weight gradients of the skinny layers in one launch: colour-1 (3 rows over the 128
+// colour-0 outputs, A = the r, g, b of dpre) and density (1 row over layer 7's 256 outputs,
+// A = dpre's sigma); partial[split][m][n] = sum over the split's samples of A[p][m] * B[p][n]
+// and the bias partials sum_p A[p][m].  Per sample phase (every 4th sample of the split) one
+// wave takes the colour columns (two per lane, float2 loads) and one the density columns
+// (four per lane, float4 loads), so no wave diverges; the four phase sums are then added in
+// a fixed order.  HBM-bound: dpre, the colour-0 rows and layer 7's rows are read once.
+__global__ __launch_bounds__(512) void skinny_wgrad_kernel(const f32x4* __restrict__ dpre,
+                                                           const float* __restrict__ hc, int ldh,
+                                                           const float* __restrict__ h7, long P, int chunk,
+                                                           float* __restrict__ pc, float* __restrict__ pcb,
+                                                           float* __restrict__ pd, float* __restrict__ pdb) {
+  __shared__ float red[4][4][256];   // [phase][colour row 0-2 | density 3][column]
   __shared__ float bred[4][4];
-  const int split = blockIdx.x, n = threadIdx.x & 255, ph = threadIdx.x >> 8;
+  const int split = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ph = wv >> 1;
+  const bool colour = (wv & 1) == 0;                       // wave-uniform
   const long p0 = long(split) * chunk;
   const long p1 = p0 + chunk < P ? p0 + chunk : P;
-  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float acc[3][4] = {}, bs[4] = {};
 #pragma unroll 4
   for (long p = p0 + ph; p < p1; p += 4) {
-    const float b = n < N ? B[p * ldb + n] : 0.0f;
+    const f32x4 a = dpre[p];
+    if (colour) {
+      const f32x2_t b = *(const f32x2_t*)(hc + p * ldh + 2 * lane);
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-      if (m < M) {
-        const float a = A[p * lda + m];
-        acc[m] = fmaf(a, b, acc[m]);
-        bs[m] = __fadd_rn(bs[m], a);
+      for (int m = 0; m < 3; ++m) {
+        acc[m][0] = fmaf(a[m], b[0], acc[m][0]);
+        acc[m][1] = fmaf(a[m], b[1], acc[m][1]);
+        bs[m] = __fadd_rn(bs[m], a[m]);
       }
+    } else {
+      const f32x4 b = ld4(h7 + p * kH + 4 * lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[0][j] = fmaf(a[3], b[j], acc[0][j]);
+      bs[3] = __fadd_rn(bs[3], a[3]);
+    }
   }
+  if (colour) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m) red[ph][m][n] = acc[m];
-  if (n == 0)
+    for (int m = 0; m < 3; ++m) *(f32x2_t*)&red[ph][m][2 * lane] = f32x2_t{acc[m][0], acc[m][1]};
+    if (lane == 0)
 #pragma unroll
-    for (int m = 0; m < 4; ++m) bred[ph][m] = bs[m];
+      for (int m = 0; m < 3; ++m) bred[ph][m] = bs[m];
+  } else {
+    *(f32x4*)&red[ph][3][4 * lane] = f32x4{acc[0][0], acc[0][1], acc[0][2], acc[0][3]};
+    if (lane == 0) bred[ph][3] = bs[3];
+  }
   __syncthreads();
-  if (ph == 0) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      if (m < M) {
-        if (n < N)
-          part[(long(split) * M + m) * N + n] =
-              __fadd_rn(__fadd_rn(red[0][m][n], red[1][m][n]), __fadd_rn(red[2][m][n], red[3][m][n]));
-        if (n == 0)
-          bpart[long(split) * M + m] = __fadd_rn(__fadd_rn(bred[0][m], bred[1][m]), __fadd_rn(bred[2][m], bred[3][m]));
-      }
-  }
+  const int t = threadIdx.x;
+  auto sum4 = [&](int m, int n) {
+    return __fadd_rn(__fadd_rn(red[0][m][n], red[1][m][n]), __fadd_rn(red[2][m][n], red[3][m][n]));
+  };
+  if (t < 3 * kC0) pc[long(split) * 3 * kC0 + t] = sum4(t / kC0, t % kC0);
+  else if (t < 3 * kC0 + 3) pcb[long(split) * 3 + (t - 3 * kC0)] =
+      __fadd_rn(__fadd_rn(bred[0][t - 3 * kC0], bred[1][t - 3 * kC0]), __fadd_rn(bred[2][t - 3 * kC0], bred[3][t - 3 * kC0]));
+  if (t < kH) pd[long(split) * kH + t] = sum4(3, t);
+  if (t == kH) pdb[split] = __fadd_rn(__fadd_rn(bred[0][3], bred[1][3]), __fadd_rn(bred[2][3], bred[3][3]));
 }
 
 // Sum of squares of all gradients (double), per block.
@@ -1233,11 +1248,9 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   for (int l = 7; l >= 0; --l) jl[l] = plan_wjob(kH, kTrunkIn[l], P, want[l], cur);
   WJob jh = plan_wjob(kC0, kHeadK, P, want[8], cur);
   if ((rc = grow_buf(tr->part, tr->part_cap, cur, "gradient partials")) != NERF_OK) return rc;
-  hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jc1.splits), dim3(1024), 0, s, (const float*)a.dpre, 4, 3,
-                     (const float*)a.hc, kHeadLd, kC0, P, kSkinnyChunk, tr->part + jc1.off, tr->part + jc1.boff);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jd.splits), dim3(1024), 0, s, (const float*)a.dpre + 3, 4, 1,
-                     (const float*)a.h[7], kH, kH, P, kSkinnyChunk, tr->part + jd.off, tr->part + jd.boff);
+  hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jc1.splits), dim3(512), 0, s, (const f32x4*)a.dpre,
+                     (const float*)a.hc, kHeadLd, (const float*)a.h[7], P, kSkinnyChunk, tr->part + jc1.off,
+                     tr->part + jc1.boff, tr->part + jd.off, tr->part + jd.boff);
   HIP_TRY(hipGetLastError());
   {
     // dZ_7 .. dZ_0 in one launch (the head's and layers 7..1's data gradients with the ReLU bits)
