@@ -13,7 +13,7 @@ for group in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU
              "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $group -T --output-format csv \
-    --kernel-include-regex "wgrad_gemm_kernel|train_fwd_kernel|train_bwd_kernel" \
+    --kernel-include-regex "wgrad_group_kernel|train_fwd_kernel|train_bwd_kernel" \
     -d "$OUT/p$i" -o run -- python3 $ROOT/tools/train_profile.py 2 > "$OUT/p$i.log" 2>&1 || exit $?
 done
 echo "sq train done"
