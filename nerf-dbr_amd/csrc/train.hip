@@ -517,21 +517,34 @@ constexpr int f32_layer_offset_t() {
 // live in registers anyway) go as a row of this lane's sample; one 16-B piece is
 // stored after each k-step group's weight loads are issued, so no weight load of this
 // layer waits behind more than one store (vmcnt counts loads and stores in issue order).
-template <int L, int NT, int NEXT>
+// Weight fragments run one k-step group ahead: pf holds this layer's group 0 on entry
+// (loaded during the previous layer's last group) and the next layer's (LN; -1: none) on
+// exit, so a group's loads have a whole group of MFMAs (2,048 cycles) to arrive and the
+// layer boundary's ReLU and bit work overlaps the next layer's first loads.
+template <int L, int NT, int NEXT, int LN, int NTN>
 __device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)[8], const float (&ext)[NEXT],
                                           const f32x4* __restrict__ blob, const float* __restrict__ prm, int lane,
-                                          int h, float* __restrict__ prev_row = nullptr) {
+                                          int h, f32x4 (&pf)[8], float* __restrict__ prev_row = nullptr) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 2;
   constexpr int KU = ksteps_f32(L);
+  constexpr int G = KU / 4;
   static_assert(KU == KH + (sh.extra == kNone ? 0 : NEXT), "layer/ext mismatch");
   load_bias<NT>(acc, prm, L, h);
   const f32x4* a_base = blob + f32_layer_offset_t<L>() / 4 + lane;
+  f32x4 a[2][NT];
 #pragma unroll
-  for (int ug = 0; ug < KU / 4; ++ug) {
-    f32x4 a[NT];
+  for (int o = 0; o < NT; ++o) a[0][o] = pf[o];
 #pragma unroll
-    for (int o = 0; o < NT; ++o) a[o] = a_base[(ug * NT + o) * 64];
+  for (int ug = 0; ug < G; ++ug) {
+    if (ug + 1 < G) {
+#pragma unroll
+      for (int o = 0; o < NT; ++o) a[(ug + 1) & 1][o] = a_base[((ug + 1) * NT + o) * 64];
+    } else if (LN >= 0) {
+      const f32x4* n_base = blob + f32_layer_offset_t<(LN >= 0 ? LN : 0)>() / 4 + lane;
+#pragma unroll
+      for (int o = 0; o < NTN; ++o) pf[o] = n_base[o * 64];
+    }
     if (KH > 0 && ug < KH / 4 && prev_row != nullptr) {
       const int t = ug >> 2, j = ug & 3;
       *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
@@ -542,7 +555,7 @@ __device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)
       const int u = 4 * ug + i;
       const float b = u < KH ? prev[u >> 4][u & 15] : ext[u - KH];
 #pragma unroll
-      for (int o = 0; o < NT; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[o][i], b, acc[o], 0, 0, 0);
+      for (int o = 0; o < NT; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ug & 1][o][i], b, acc[o], 0, 0, 0);
     }
   }
 }
@@ -591,6 +604,9 @@ __global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restri
   const long p = (long(blockIdx.x) * 4 + wave) * kSamplesPerWave + (lane & 31);
   const bool valid = p < n_points;
   const long pc = valid ? p : n_points - 1;
+  f32x4 pf[8];                      // layer 0's first weight fragments, in flight during the encoding
+#pragma unroll
+  for (int o = 0; o < 8; ++o) pf[o] = blob[lane + o * 64];
   float x[3], d[3];
   fetch_sample<false>(src, pc, x, d);
   float pe[32], de[16];
@@ -601,32 +617,32 @@ __global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restri
   float* const nul = nullptr;
 #define ROW(l) (valid ? o.h[l] + p * kH : nul)
 #define BITS(acc, l) store_bits(acc, o.mb[l] + p * (kH / 32), h, valid && h == 0)
-  fwd_layer<L0, 8, 32>(a, b, pe, blob, prm, lane, h);
+  fwd_layer<L0, 8, 32, L1, 8>(a, b, pe, blob, prm, lane, h, pf);
   relu_tiles<8>(a);
   BITS(a, 0);
-  fwd_layer<L1, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(0));
+  fwd_layer<L1, 8, 32, L2, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(0));
   relu_tiles<8>(b);
   BITS(b, 1);
-  fwd_layer<L2, 8, 32>(a, b, pe, blob, prm, lane, h, ROW(1));
+  fwd_layer<L2, 8, 32, L3, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(1));
   relu_tiles<8>(a);
   BITS(a, 2);
-  fwd_layer<L3, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(2));
+  fwd_layer<L3, 8, 32, L4, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(2));
   relu_tiles<8>(b);
   BITS(b, 3);
-  fwd_layer<L4, 8, 32>(a, b, pe, blob, prm, lane, h, ROW(3));   // skip: [x, pe] (nerf.py:109-110)
+  fwd_layer<L4, 8, 32, L5, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(3));   // skip: [x, pe] (nerf.py:109-110)
   relu_tiles<8>(a);
   BITS(a, 4);
-  fwd_layer<L5, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(4));
+  fwd_layer<L5, 8, 32, L6, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(4));
   relu_tiles<8>(b);
   BITS(b, 5);
-  fwd_layer<L6, 8, 32>(a, b, pe, blob, prm, lane, h, ROW(5));
+  fwd_layer<L6, 8, 32, L7, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(5));
   relu_tiles<8>(a);
   BITS(a, 6);
-  fwd_layer<L7, 8, 32>(b, a, pe, blob, prm, lane, h, ROW(6));
+  fwd_layer<L7, 8, 32, C0, 4>(b, a, pe, blob, prm, lane, h, pf, ROW(6));
   relu_tiles<8>(b);
   BITS(b, 7);
   const float sigma = density_head(b, prm, h);
-  fwd_layer<C0, 4, 16>(a, b, de, blob, prm, lane, h, ROW(7));   // [x, PE4(d)] (nerf.py:117-121)
+  fwd_layer<C0, 4, 16, -1, 0>(a, b, de, blob, prm, lane, h, pf, ROW(7));   // [x, PE4(d)] (nerf.py:117-121)
 #undef ROW
 #undef BITS
   relu_tiles<4>(a);
@@ -646,21 +662,31 @@ __global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restri
 // from the head's pre-activation gradient rows [P][132] (colour-0, density); writes dZ_l
 // rows [P][256] for l = 7..0 (the weight gradients' A operand), each stored piecewise
 // during the following layer as in the forward.
+// Weight fragments one k-step group ahead as in fwd_layer: pf holds this layer's group 0
+// on entry and the next backward layer's (its blob at next_blob; nullptr: none) on exit.
 template <int KU>
 __device__ __forceinline__ void bwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)[8], float dens,
-                                          const f32x4* __restrict__ blob, int lane, int h,
-                                          float* __restrict__ prev_row) {
+                                          const f32x4* __restrict__ blob, const f32x4* __restrict__ next_blob,
+                                          int lane, int h, f32x4 (&pf)[8], float* __restrict__ prev_row) {
   constexpr int KH = KU == kHeadBwdKsteps ? kC0 / 2 : KU;   // k-steps fed by prev; the head's next is the density
+  constexpr int G = KU / 4;
 #pragma unroll
   for (int o = 0; o < 8; ++o)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[o][r] = 0.0f;
   const f32x4* a_base = blob + lane;
+  f32x4 a[2][8];
 #pragma unroll
-  for (int ug = 0; ug < KU / 4; ++ug) {
-    f32x4 a[8];
+  for (int o = 0; o < 8; ++o) a[0][o] = pf[o];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) a[o] = a_base[(ug * 8 + o) * 64];
+  for (int ug = 0; ug < G; ++ug) {
+    if (ug + 1 < G) {
+#pragma unroll
+      for (int o = 0; o < 8; ++o) a[(ug + 1) & 1][o] = a_base[((ug + 1) * 8 + o) * 64];
+    } else if (next_blob != nullptr) {
+#pragma unroll
+      for (int o = 0; o < 8; ++o) pf[o] = next_blob[lane + o * 64];
+    }
     if (prev_row != nullptr && ug < 32) {     // 256-wide dZ rows: 32 pieces of 16 B
       const int t = ug >> 2, j = ug & 3;
       *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
@@ -671,7 +697,7 @@ __device__ __forceinline__ void bwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)
       const int u = 4 * ug + i;
       const float b = u < KH ? prev[u >> 4][u & 15] : (u == KH && h == 0 ? dens : 0.0f);
 #pragma unroll
-      for (int o = 0; o < 8; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[o][i], b, acc[o], 0, 0, 0);
+      for (int o = 0; o < 8; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ug & 1][o][i], b, acc[o], 0, 0, 0);
     }
   }
 }
@@ -698,6 +724,9 @@ __global__ __launch_bounds__(256, 1) void train_bwd_kernel(const f32x4* __restri
   const long p = (long(blockIdx.x) * 4 + wave) * kSamplesPerWave + (lane & 31);
   const bool valid = p < n_points;
   const long pc = valid ? p : n_points - 1;
+  f32x4 pf[8];                      // the head's first weight fragments, in flight during the row loads
+#pragma unroll
+  for (int o = 0; o < 8; ++o) pf[o] = blob[bwd_layer_offset(0) / 4 + lane + o * 64];
   f32x16 a[8], b[8];
   // the head's gradient rows as a 4-tile "accumulator" (feature 32t + acc_row(r, h))
   const float* row = io.dhc + pc * kHeadLd;
@@ -719,29 +748,31 @@ __global__ __launch_bounds__(256, 1) void train_bwd_kernel(const f32x4* __restri
   float* const nul = nullptr;
 #define DZ(l) (valid ? io.dz[l] + p * kH : nul)
   load_bits(7);
-  bwd_layer<kHeadBwdKsteps>(a, b, dens, blob + bwd_layer_offset(0) / 4, lane, h, nul);
+#define BLOB(b) (blob + bwd_layer_offset(b) / 4)
+  bwd_layer<kHeadBwdKsteps>(a, b, dens, BLOB(0), BLOB(1), lane, h, pf, nul);
   apply_bits(a, w, h);                                              // dZ_7
   load_bits(6);
-  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(1) / 4, lane, h, DZ(7));
+  bwd_layer<128>(b, a, 0.0f, BLOB(1), BLOB(2), lane, h, pf, DZ(7));
   apply_bits(b, w, h);                                              // dZ_6
   load_bits(5);
-  bwd_layer<128>(a, b, 0.0f, blob + bwd_layer_offset(2) / 4, lane, h, DZ(6));
+  bwd_layer<128>(a, b, 0.0f, BLOB(2), BLOB(3), lane, h, pf, DZ(6));
   apply_bits(a, w, h);                                              // dZ_5
   load_bits(4);
-  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(3) / 4, lane, h, DZ(5));
+  bwd_layer<128>(b, a, 0.0f, BLOB(3), BLOB(4), lane, h, pf, DZ(5));
   apply_bits(b, w, h);                                              // dZ_4
   load_bits(3);
-  bwd_layer<128>(a, b, 0.0f, blob + bwd_layer_offset(4) / 4, lane, h, DZ(4));   // layer 4's hidden inputs
+  bwd_layer<128>(a, b, 0.0f, BLOB(4), BLOB(5), lane, h, pf, DZ(4));   // layer 4's hidden inputs
   apply_bits(a, w, h);                                              // dZ_3
   load_bits(2);
-  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(5) / 4, lane, h, DZ(3));
+  bwd_layer<128>(b, a, 0.0f, BLOB(5), BLOB(6), lane, h, pf, DZ(3));
   apply_bits(b, w, h);                                              // dZ_2
   load_bits(1);
-  bwd_layer<128>(a, b, 0.0f, blob + bwd_layer_offset(6) / 4, lane, h, DZ(2));
+  bwd_layer<128>(a, b, 0.0f, BLOB(6), BLOB(7), lane, h, pf, DZ(2));
   apply_bits(a, w, h);                                              // dZ_1
   load_bits(0);
-  bwd_layer<128>(b, a, 0.0f, blob + bwd_layer_offset(7) / 4, lane, h, DZ(1));
+  bwd_layer<128>(b, a, 0.0f, BLOB(7), nullptr, lane, h, pf, DZ(1));
   apply_bits(b, w, h);                                              // dZ_0
+#undef BLOB
   if (valid) store_rows<8>(b, io.dz[0] + p * kH, h);
 #undef DZ
 }
