@@ -254,7 +254,9 @@ void nerf_trainer_destroy(nerf_trainer* tr);
  *   select  device int32 [n_rays] = torch.randperm(height*width)[:n_rays] (trainer.py:111);
  *   t_rand  device [n_rays][n_coarse] = the coarse pass's torch.rand_like (rendering.py:47).
  * loss_out (device [3], may be NULL): loss, coarse MSE, fine MSE.  flags: NERF_TRAIN_NO_UPDATE
- * stops after backward (gradients unclipped, no optimizer or schedule step). */
+ * stops after backward (gradients unclipped, no optimizer or schedule step).  Work is queued on
+ * `stream`; a call on another stream than the trainer's previous call waits for that call's
+ * work (the trainer's workspace and state are shared by all its calls). */
 #define NERF_TRAIN_NO_UPDATE 1
 int nerf_train_step(nerf_trainer* tr, const float* image, int height, int width, float focal,
                     const float* c2w, const int32_t* select, int n_rays, const float* t_rand, int flags,

@@ -1080,6 +1080,11 @@ struct nerf_trainer {
   bool have_times = false;
   hipEvent_t ev[12] = {};
   double gemm_flops = 0.0;
+  // stream ordering: the workspace and state are reused by every call, so a call on a
+  // stream other than the last one's waits for the last call's work (done)
+  hipEvent_t done = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool pending = false;
 };
 
 namespace {
@@ -1455,6 +1460,8 @@ int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* c
     return fail(set_error(NERF_E_HIP, "trainer z upload failed"));
   for (auto& e : tr->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(set_error(NERF_E_HIP, "hipEventCreate"));
+  if (hipEventCreateWithFlags(&tr->done, hipEventDisableTiming) != hipSuccess)
+    return fail(set_error(NERF_E_HIP, "hipEventCreate"));
   hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, 0, (const float*)tr->params,
                      tr->gemmw);
   if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -1472,12 +1479,25 @@ void nerf_trainer_destroy(nerf_trainer* tr) {
   if (tr->bad) (void)hipFree(tr->bad);
   for (auto& e : tr->ev)
     if (e) (void)hipEventDestroy(e);
+  if (tr->done) (void)hipEventDestroy(tr->done);
   delete tr;
 }
 
 }  // extern "C"
 
 namespace {
+
+// A call on a different stream than the previous call's waits for that call's work.
+int order_after_last(nerf_trainer* tr, hipStream_t s) {
+  if (tr->pending && s != tr->last_stream) HIP_TRY(hipStreamWaitEvent(s, tr->done, 0));
+  return NERF_OK;
+}
+int record_done(nerf_trainer* tr, hipStream_t s) {
+  HIP_TRY(hipEventRecord(tr->done, s));
+  tr->last_stream = s;
+  tr->pending = true;
+  return NERF_OK;
+}
 
 int train_impl(nerf_trainer* tr, const float* image, int height, int width, float focal, const float* c2w,
                const int32_t* select, int n_rays, int n_total, const float* t_rand, bool update, float* loss_out,
@@ -1503,6 +1523,7 @@ int train_impl(nerf_trainer* tr, const float* image, int height, int width, floa
   float* target = rays_d + 3 * size_t(n_rays);
   float* zc = tr->ws + al64(size_t(n_rays) * 9);
   float* loss_ray = zc + al64(size_t(n_rays) * tr->cfg.n_coarse);
+  if ((rc = order_after_last(tr, s)) != NERF_OK) return rc;
   tr->have_times = false;
   tr->gemm_flops = 0.0;
   auto mark = [&](int i) -> int {
@@ -1535,7 +1556,7 @@ int train_impl(nerf_trainer* tr, const float* image, int height, int width, floa
   if (update && (rc = update_impl(tr, s)) != NERF_OK) return rc;
   if ((rc = mark(11)) != NERF_OK) return rc;
   tr->have_times = tr->profiling;
-  return NERF_OK;
+  return record_done(tr, s);
 }
 
 }  // namespace
@@ -1569,7 +1590,10 @@ int nerf_trainer_set_grad_buffer(nerf_trainer* tr, float* grads_dev) {
 int nerf_trainer_update(nerf_trainer* tr, void* stream) {
   if (!tr) return set_error(NERF_E_INVALID, "null trainer");
   DeviceGuardT dg(tr->device);
-  return update_impl(tr, (hipStream_t)stream);
+  const hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = order_after_last(tr, s)) != NERF_OK || (rc = update_impl(tr, s)) != NERF_OK) return rc;
+  return record_done(tr, s);
 }
 
 int nerf_trainer_read(nerf_trainer* tr, int what, int net, float* const* host_out, int n_params) {

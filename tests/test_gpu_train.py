@@ -237,3 +237,26 @@ def test_train_backward_shares_sum_to_the_full_step(fx):
             d = np.abs(pa[k].astype(np.float64) - pb[k])
             # Adam's first step is lr * sign(g): equal except where g sits at rounding level
             assert np.mean(d <= 1e-7 + 1e-6 * np.abs(pb[k])) >= 0.999, (net, k)
+
+
+def test_train_steps_on_two_streams_match_one_stream(fx):
+    """A step queued on another stream than the previous one waits for it (the trainer's
+    workspace is shared): two steps on two streams give the same parameters, bit for bit,
+    as the same two steps on one stream (every kernel of the step is deterministic)."""
+    n = int(fx["n_rays"])
+    ref, _ = _trainer(n)
+    two, _ = _trainer(n)
+    side = torch.cuda.Stream()
+    for s in range(2):
+        sel, tr = fx[f"step{s}_select"].astype(np.int32), fx[f"step{s}_t_rand"]
+        ref.train_step(_batch(fx), select_inds=sel, t_rand=tr, sync=False)
+        if s == 0:
+            two.train_step(_batch(fx), select_inds=sel, t_rand=tr, sync=False)
+        else:
+            with torch.cuda.stream(side):
+                two.train_step(_batch(fx), select_inds=sel, t_rand=tr, sync=False)
+    torch.cuda.synchronize()
+    for net in (0, 1):
+        pa, pb = ref.state_dicts()[net], two.state_dicts()[net]
+        for k in T.PARAM_ORDER:
+            assert np.array_equal(pa[k], pb[k]), (net, k)
