@@ -1085,6 +1085,10 @@ struct nerf_trainer {
   hipEvent_t done = nullptr;
   hipStream_t last_stream = nullptr;
   bool pending = false;
+  // the coarse net's pass runs on a second stream beside the fine net's (they share only
+  // the rays): fork after the rays and samples, join before the loss and the update
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 namespace {
@@ -1154,9 +1158,6 @@ Acts carve_acts(float* base, long P) {
   return a;
 }
 
-// One column tile spans all of N (128, 256 or 320 columns) and one row tile all of M, so
-// each operand row is read once, all over 8 waves: 256 x {128, 256, 320} (trunk layers 0
-// (63 columns), 1-3 / 5-7, 4 (319)), 128 x 384 (the colour-0 layer, 283).
 // The four weight-gradient shapes of a NeRFModel (M x N: B's sources)
 //   256 x 256: the previous layer's rows; 256 x 319: [layer 3's rows, the position
 //   encodings]; 256 x 63: the position encodings; 128 x 283: [layer 7's rows, the direction
@@ -1227,11 +1228,40 @@ double gemm_macs_per_sample() {
   return 2.0 * fwd + bwd_data;                            // forward, weight grads, data grads
 }
 
-// Forward + backward of one net on P = n_rays * S samples; gradients into grads (flat).
+// The weight-gradient partials of one net's pass over P samples: the skinny layers' (one
+// split per kSkinnyChunk samples) and the nine GEMM jobs'; floats = the buffer size.
+constexpr int kSkinnyChunk = 256;   // samples per block of the skinny weight-gradient kernel
+struct PartPlan {
+  WJob jc1, jd, jl[8], jh;
+  size_t floats;
+};
+PartPlan plan_parts(long P) {
+  PartPlan pp;
+  size_t cur = 0;
+  const int sk_splits = int(blocks_for(P, kSkinnyChunk));
+  pp.jc1 = WJob{3, kC0, sk_splits, kSkinnyChunk, 0, 0};
+  pp.jd = WJob{1, kH, sk_splits, kSkinnyChunk, 0, 0};
+  for (WJob* j : {&pp.jc1, &pp.jd}) {
+    j->off = cur;
+    cur += al64(size_t(j->splits) * j->M * j->N);
+    j->boff = cur;
+    cur += al64(size_t(j->splits) * j->M);
+  }
+  int want[kMaxWJobs];
+  wgrad_splits(want);
+  for (int l = 7; l >= 0; --l) pp.jl[l] = plan_wjob(kH, kTrunkIn[l], P, want[l], cur);
+  pp.jh = plan_wjob(kC0, kHeadK, P, want[8], cur);
+  pp.floats = cur;
+  return pp;
+}
+
+// Forward + backward of one net on P = n_rays * S samples, in its own activation region
+// (acts) and partials buffer (part, plan_parts(P).floats); gradients into grads (flat).
 int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d, const float* target,
-             const float* z, int z_stride, int n_rays, int n_total, int S, float* loss_ray, hipStream_t s, int ev0) {
+             const float* z, int z_stride, int n_rays, int n_total, int S, float* loss_ray, hipStream_t s, int ev0,
+             float* acts, float* part) {
   const long P = long(n_rays) * S;
-  Acts a = carve_acts(tr->ws + head_floats(n_rays, tr->cfg.n_coarse), P);
+  Acts a = carve_acts(acts, P);
   const float* prm = tr->params + net * kNetFloats;
   const float* gw = tr->gemmw + net * kGemmFloats;
   float* grads = tr->grads + net * kNetFloats;
@@ -1268,25 +1298,12 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   if ((rc = mark(3)) != NERF_OK) return rc;
 
   // backward GEMMs; weight gradients as split partials
-  size_t cur = 0;
-  constexpr int kSkinnyChunk = 256;   // samples per block of the skinny weight-gradient kernel
-  const int sk_splits = int(blocks_for(P, kSkinnyChunk));
-  WJob jc1{3, kC0, sk_splits, kSkinnyChunk, 0, 0}, jd{1, kH, sk_splits, kSkinnyChunk, 0, 0};
-  for (WJob* j : {&jc1, &jd}) {
-    j->off = cur;
-    cur += al64(size_t(j->splits) * j->M * j->N);
-    j->boff = cur;
-    cur += al64(size_t(j->splits) * j->M);
-  }
-  int want[kMaxWJobs];
-  wgrad_splits(want);
-  WJob jl[8];
-  for (int l = 7; l >= 0; --l) jl[l] = plan_wjob(kH, kTrunkIn[l], P, want[l], cur);
-  WJob jh = plan_wjob(kC0, kHeadK, P, want[8], cur);
-  if ((rc = grow_buf(tr->part, tr->part_cap, cur, "gradient partials")) != NERF_OK) return rc;
+  const PartPlan pp = plan_parts(P);
+  const WJob &jc1 = pp.jc1, &jd = pp.jd, &jh = pp.jh;
+  const WJob* jl = pp.jl;
   hipLaunchKernelGGL(skinny_wgrad_kernel, dim3(jc1.splits), dim3(512), 0, s, (const f32x4*)a.dpre,
-                     (const float*)a.hc, kHeadLd, (const float*)a.h[7], P, kSkinnyChunk, tr->part + jc1.off,
-                     tr->part + jc1.boff, tr->part + jd.off, tr->part + jd.boff);
+                     (const float*)a.hc, kHeadLd, (const float*)a.h[7], P, kSkinnyChunk, part + jc1.off,
+                     part + jc1.boff, part + jd.off, part + jd.boff);
   HIP_TRY(hipGetLastError());
   {
     // dZ_7 .. dZ_0 in one launch (the head's and layers 7..1's data gradients with the ReLU bits)
@@ -1306,8 +1323,8 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
       g.M = j.M, g.N = j.N, g.K = int(P);
       g.a = Src2{A, nullptr, lda, 0, 0x7fffffff};
       g.b = B;
-      g.c = tr->part + j.off, g.ldc = j.N;
-      g.bias_part = tr->part + j.boff;
+      g.c = part + j.off, g.ldc = j.N;
+      g.bias_part = part + j.boff;
       g.k_split = j.k_split;
       g.c_split = long(j.M) * j.N;
       if ((grp.shape[grp.n] = wgrad_shape(g)) < 0) return false;
@@ -1334,7 +1351,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   RedJobs jobs{};
   auto job = [&](int i, const WJob& j, int r1, long w0, long b0, int ld0, int nw0, long w1, long b1, int ld1,
                  int nw1) {
-    jobs.j[i] = RedJob{tr->part + j.off, tr->part + j.boff, j.splits, j.M, j.N, r1, w0, b0, ld0, nw0, w1, b1, ld1, nw1};
+    jobs.j[i] = RedJob{part + j.off, part + j.boff, j.splits, j.M, j.N, r1, w0, b0, ld0, nw0, w1, b1, ld1, nw1};
   };
   long maxe = 0;
   for (int l = 0; l < 8; ++l) {
@@ -1460,8 +1477,11 @@ int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* c
     return fail(set_error(NERF_E_HIP, "trainer z upload failed"));
   for (auto& e : tr->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(set_error(NERF_E_HIP, "hipEventCreate"));
-  if (hipEventCreateWithFlags(&tr->done, hipEventDisableTiming) != hipSuccess)
-    return fail(set_error(NERF_E_HIP, "hipEventCreate"));
+  if (hipEventCreateWithFlags(&tr->done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&tr->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&tr->join, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&tr->side, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_error(NERF_E_HIP, "trainer events / stream"));
   hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, 0, (const float*)tr->params,
                      tr->gemmw);
   if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -1479,7 +1499,9 @@ void nerf_trainer_destroy(nerf_trainer* tr) {
   if (tr->bad) (void)hipFree(tr->bad);
   for (auto& e : tr->ev)
     if (e) (void)hipEventDestroy(e);
-  if (tr->done) (void)hipEventDestroy(tr->done);
+  for (hipEvent_t e : {tr->done, tr->fork, tr->join})
+    if (e) (void)hipEventDestroy(e);
+  if (tr->side) (void)hipStreamDestroy(tr->side);
   delete tr;
 }
 
@@ -1512,18 +1534,22 @@ int train_impl(nerf_trainer* tr, const float* image, int height, int width, floa
   if (long(n_rays) * Smax > 0x7fffffffL / 2) return set_error(NERF_E_INVALID, "nerf_train_step: too many samples");
   DeviceGuardT dg(tr->device);
   hipStream_t s = (hipStream_t)stream;
-  const long Pmax = long(n_rays) * Smax;
+  const long Pc = long(n_rays) * tr->cfg.n_coarse, Pf = long(n_rays) * tr->cfg.n_fine;
   // workspace: rays_o, rays_d, targets [n_rays][3] each | coarse z [n_rays][n_coarse] |
-  // per-ray squared errors [2][n_rays] | one net's activations (net_pass)
+  // per-ray squared errors [2][n_rays] | the coarse net's activations | the fine net's;
+  // partials: the coarse net's | the fine net's (both nets' passes may run at once)
   const size_t head = head_floats(n_rays, tr->cfg.n_coarse);
+  const size_t acts_c = acts_floats(Pc), parts_c = plan_parts(Pc).floats;
   int rc;
-  if ((rc = grow_buf(tr->ws, tr->ws_cap, head + acts_floats(Pmax) + 64, "training workspace")) != NERF_OK) return rc;
+  if ((rc = order_after_last(tr, s)) != NERF_OK) return rc;
+  if ((rc = grow_buf(tr->ws, tr->ws_cap, head + acts_c + acts_floats(Pf) + 64, "training workspace")) != NERF_OK ||
+      (rc = grow_buf(tr->part, tr->part_cap, parts_c + plan_parts(Pf).floats, "gradient partials")) != NERF_OK)
+    return rc;
   float* rays_o = tr->ws;
   float* rays_d = rays_o + 3 * size_t(n_rays);
   float* target = rays_d + 3 * size_t(n_rays);
   float* zc = tr->ws + al64(size_t(n_rays) * 9);
   float* loss_ray = zc + al64(size_t(n_rays) * tr->cfg.n_coarse);
-  if ((rc = order_after_last(tr, s)) != NERF_OK) return rc;
   tr->have_times = false;
   tr->gemm_flops = 0.0;
   auto mark = [&](int i) -> int {
@@ -1542,13 +1568,24 @@ int train_impl(nerf_trainer* tr, const float* image, int height, int width, floa
   HIP_TRY(hipGetLastError());
   // coarse samples stratified with the injected draw (rendering.py:42-47)
   HIP_TRY(launch_sample(tr->ztab, t_rand, n_rays, tr->cfg.n_coarse, nullptr, nullptr, zc, nullptr, s));
+  // the two nets' passes: concurrently (coarse on the side stream), or one after the other
+  // on the caller's stream when profiling (the stage events time one pass at a time)
+  const bool concurrent = !tr->profiling;
+  hipStream_t sc = s;
+  if (concurrent) {
+    HIP_TRY(hipEventRecord(tr->fork, s));
+    HIP_TRY(hipStreamWaitEvent(tr->side, tr->fork, 0));
+    sc = tr->side;
+  }
   if ((rc = net_pass(tr, 0, rays_o, rays_d, target, zc, tr->cfg.n_coarse, n_rays, n_total, tr->cfg.n_coarse, loss_ray,
-                     s, 0)) != NERF_OK)
+                     sc, 0, tr->ws + head, tr->part)) != NERF_OK)
     return rc;
+  if (concurrent) HIP_TRY(hipEventRecord(tr->join, sc));
   if ((rc = mark(5)) != NERF_OK) return rc;
   if ((rc = net_pass(tr, 1, rays_o, rays_d, target, tr->ztab + 1024, 0, n_rays, n_total, tr->cfg.n_fine,
-                     loss_ray + n_rays, s, 5)) != NERF_OK)
+                     loss_ray + n_rays, s, 5, tr->ws + head + acts_c, tr->part + parts_c)) != NERF_OK)
     return rc;
+  if (concurrent) HIP_TRY(hipStreamWaitEvent(s, tr->join, 0));
   if ((rc = mark(10)) != NERF_OK) return rc;
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)loss_ray, n_rays, n_total,
                      (const double*)nullptr, 0, 0.0f, loss_out, (float*)nullptr);

@@ -40,6 +40,14 @@ class Lib:
             self.lib.nerf_last_error()
         self.lib.nerf_trainer_set_profiling(self.h, 1)
 
+    def set_profiling(self, on):
+        self.lib.nerf_trainer_set_profiling(self.h, 1 if on else 0)
+
+    def run(self, image, pose, sel, tr):
+        rc = self.lib.nerf_train_step(self.h, image.data_ptr(), image.shape[0], image.shape[1], 555.6,
+                                      rt._fptr(pose), sel.data_ptr(), sel.numel(), tr.data_ptr(), 0, None, 0)
+        assert rc == 0, self.lib.nerf_last_error()
+
     def step(self, image, pose, sel, tr):
         rc = self.lib.nerf_train_step(self.h, image.data_ptr(), image.shape[0], image.shape[1], 555.6,
                                       rt._fptr(pose), sel.data_ptr(), sel.numel(), tr.data_ptr(), 0, None, 0)
@@ -52,6 +60,9 @@ class Lib:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--wall", type=int, default=0,
+                    help="also time this many back-to-back steps per library per round, profiling off "
+                         "(wall clock on the stream: the trainer may overlap its two nets' passes)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     cfg = rt.TrainConfig()
@@ -72,6 +83,22 @@ def main():
     for _ in range(a.rounds):
         for l in libs:
             res[l.path].append(l.step(image, pose, sel, tr))
+    if a.wall:
+        wall = {l.path: [] for l in libs}
+        for l in libs:
+            l.set_profiling(False)
+        for _ in range(a.rounds):
+            for l in libs:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(a.wall):
+                    l.run(image, pose, sel, tr)
+                e1.record()
+                torch.cuda.synchronize()
+                wall[l.path].append(e0.elapsed_time(e1) / a.wall)
+        for p, v in wall.items():
+            print(f"{os.path.basename(p):28s} wall {np.median(v):7.3f} ms per step (min {np.min(v):.3f}), profiling off")
     for p, v in res.items():
         v = np.array(v)
         med = np.median(v, 0)
