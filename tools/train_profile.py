@@ -20,6 +20,10 @@ def main(steps=5):
     cfg = {"lr": 3e-4, "weight_decay": 1e-6, "gradient_clipping": 1.0, "n_rays": 2048}
     sd_c, sd_f = W.synthetic_models(0)
     tr = MI355XTrainer(cfg, sd_c, sd_f)
+    # profiling on: the two nets' passes run one after the other on one stream, so each
+    # kernel's trace duration is its own (unprofiled steps overlap the coarse net's pass
+    # with the fine net's on a second stream)
+    tr.set_profiling(True)
     rng = np.random.RandomState(3)
     image = torch.from_numpy(rng.rand(400, 400, 3).astype(np.float32)).cuda()
     pose = torch.eye(4)
