@@ -67,12 +67,12 @@ def _compare_grads(g_gpu, g_ref, label):
     return rels
 
 
-def _check_step_grads(gpu, orc, label):
+def _check_step_grads(gpu, orc, label, head_tol=1e-5):
     rels = _compare_grads(gpu.grads(0), orc.grads(0), (label, 0)) + _compare_grads(gpu.grads(1), orc.grads(1),
                                                                                    (label, 1))
     for i, k in enumerate(T.PARAM_ORDER * 2):
         if k.startswith(("color_layers.1", "density_head")):
-            assert rels[i] <= 1e-5, (label, i // len(T.PARAM_ORDER), k, rels[i])
+            assert rels[i] <= head_tol, (label, i // len(T.PARAM_ORDER), k, rels[i])
     return max(rels), float(np.median(rels))
 
 
@@ -165,6 +165,28 @@ def test_train_step_ragged_shapes(n_rays, n_coarse, n_fine, clip):
     ref = orc.backward(image, pose, 30.0, sel, tr)
     assert abs(loss - ref[0]) <= 1e-5 * abs(ref[0])
     _check_step_grads(gpu, orc, n_rays)
+
+
+@pytest.mark.parametrize("n_rays,n_coarse,n_fine", [(1, 8, 8), (3, 5, 7), (2, 16, 2)])
+def test_train_step_tiny_shapes(n_rays, n_coarse, n_fine):
+    """Fewer samples than one 16-row k tile (one split, rows past K zeroed), odd sample
+    counts, a two-sample fine pass.  With one to three rays nothing averages: a ray's colour
+    residual (rgb - target) and the density head's gradient sums cancel (the fine net's
+    density bias gradient is 1.4e-4 from terms ~1e-2 in the one-ray case), so the forward's
+    fp32 differences reach the heads at up to 1e-4 normwise (measured 9.5e-5 on the density
+    bias, 4.2e-5 on its weight, every other tensor <= 8.7e-6): heads bounded at 2e-4."""
+    rng = np.random.RandomState(100 + n_rays)
+    h, w = 6, 5
+    image = rng.rand(h, w, 3).astype(np.float32)
+    pose = _look_at([0.3, -3.5, 1.2])
+    sel = rng.permutation(h * w)[:n_rays]
+    tr = rng.rand(n_rays, n_coarse).astype(np.float32)
+    gpu, orc = _trainer(n_rays, {"n_coarse": n_coarse, "n_fine": n_fine})
+    batch = {"image": torch.from_numpy(image), "pose": torch.from_numpy(pose), "focal": 6.0}
+    loss = gpu.train_step(batch, select_inds=sel.astype(np.int32), t_rand=tr, update=False)
+    ref = orc.backward(image, pose, 6.0, sel, tr)
+    assert abs(loss - ref[0]) <= 1e-5 * abs(ref[0])
+    _check_step_grads(gpu, orc, (n_rays, n_coarse, n_fine), head_tol=2e-4)
 
 
 def test_train_headline_config_grads():
