@@ -513,26 +513,32 @@ constexpr int f32_layer_offset_t() {
   return off;
 }
 
-// prev_row (optional): where the previous layer's activations (this layer's B operand,
-// live in registers anyway) go as a row of this lane's sample; one 16-B piece is
-// stored after each k-step group's weight loads are issued, so no weight load of this
-// layer waits behind more than one store (vmcnt counts loads and stores in issue order).
-// Weight fragments run one k-step group ahead: pf holds this layer's group 0 on entry
-// (loaded during the previous layer's last group) and the next layer's (LN; -1: none) on
-// exit, so a group's loads have a whole group of MFMAs (2,048 cycles) to arrive and the
-// layer boundary's ReLU and bit work overlaps the next layer's first loads.
+// prev holds the previous layer's pre-activation accumulators: tile t is ReLU'd at the start
+// of k-step group 4t, the first group that reads it, together with its ReLU bit word (the
+// backward's mask), so that work runs between this layer's MFMAs instead of as a serial
+// block at the layer boundary.  prev_row (optional): where the ReLU'd activations go as a
+// row of this lane's sample, one 16-B piece per group after that group's weight loads (no
+// weight load waits behind more than one store: vmcnt counts loads and stores in issue
+// order); prev_bits (optional): the previous layer's 8 bit words for this sample, stored by
+// lane half 0 once all eight are known.  Weight fragments run one k-step group ahead: pf
+// holds this layer's group 0 on entry (loaded during the previous layer's last group) and
+// the next layer's (LN; -1: none) on exit, so a group's loads have a whole group of MFMAs
+// (2,048 cycles) to arrive.
 template <int L, int NT, int NEXT, int LN, int NTN>
-__device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)[8], const float (&ext)[NEXT],
+__device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], f32x16 (&prev)[8], const float (&ext)[NEXT],
                                           const f32x4* __restrict__ blob, const float* __restrict__ prm, int lane,
-                                          int h, f32x4 (&pf)[8], float* __restrict__ prev_row = nullptr) {
+                                          int h, f32x4 (&pf)[8], float* __restrict__ prev_row = nullptr,
+                                          unsigned* __restrict__ prev_bits = nullptr) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 2;
   constexpr int KU = ksteps_f32(L);
   constexpr int G = KU / 4;
   static_assert(KU == KH + (sh.extra == kNone ? 0 : NEXT), "layer/ext mismatch");
+  static_assert(KH == 0 || KH == 128, "hidden inputs: none or 256 features (8 tiles)");
   load_bias<NT>(acc, prm, L, h);
   const f32x4* a_base = blob + f32_layer_offset_t<L>() / 4 + lane;
   f32x4 a[2][NT];
+  unsigned wbits[8];
 #pragma unroll
   for (int o = 0; o < NT; ++o) a[0][o] = pf[o];
 #pragma unroll
@@ -545,10 +551,25 @@ __device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)
 #pragma unroll
       for (int o = 0; o < NTN; ++o) pf[o] = n_base[o * 64];
     }
+    if (KH > 0 && ug % 4 == 0 && ug < KH / 4) {   // tile t of prev: ReLU, then its bit word
+      const int t = ug / 4;
+      unsigned m = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        prev[t][r] = relu(prev[t][r]);
+        m |= (prev[t][r] > 0.0f ? 1u : 0u) << acc_row(r, h);
+      }
+      const auto sw = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+      wbits[t] = unsigned(sw[0]) | unsigned(sw[1]);
+    }
     if (KH > 0 && ug < KH / 4 && prev_row != nullptr) {
       const int t = ug >> 2, j = ug & 3;
       *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
           f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
+      if (ug == KH / 4 - 1 && prev_bits != nullptr && h == 0) {
+        ((u32x4_t*)prev_bits)[0] = u32x4_t{wbits[0], wbits[1], wbits[2], wbits[3]};
+        ((u32x4_t*)prev_bits)[1] = u32x4_t{wbits[4], wbits[5], wbits[6], wbits[7]};
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -568,24 +589,6 @@ __device__ __forceinline__ void store_rows(const f32x16 (&a)[8], float* __restri
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       *(f32x4*)(row + 32 * t + 8 * j + 4 * h) = f32x4{a[t][4 * j], a[t][4 * j + 1], a[t][4 * j + 2], a[t][4 * j + 3]};
-}
-
-// ReLU bits of this lane's sample, one word per 32 features (bit = feature % 32): each
-// lane half holds 16 of a tile's 32 rows; the halves' masks meet by a cross-half swap.
-__device__ __forceinline__ void store_bits(const f32x16 (&a)[8], unsigned* __restrict__ words, int h, bool store) {
-  unsigned w[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    unsigned m = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) m |= (a[t][r] > 0.0f ? 1u : 0u) << acc_row(r, h);
-    const auto sw = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-    w[t] = unsigned(sw[0]) | unsigned(sw[1]);
-  }
-  if (store) {
-    ((u32x4_t*)words)[0] = u32x4_t{w[0], w[1], w[2], w[3]};
-    ((u32x4_t*)words)[1] = u32x4_t{w[4], w[5], w[6], w[7]};
-  }
 }
 
 struct FwdOut {
@@ -613,36 +616,21 @@ __global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restri
   pos_encode(x[0], x[1], x[2], h, pe);
   dir_encode(d[0], d[1], d[2], h, de);
   f32x16 a[8], b[8];
-  // each layer's rows are stored while the next layer runs (fwd_layer prev_row); bits now
+  // each layer's ReLU, bit words and rows happen while the next layer runs (fwd_layer)
   float* const nul = nullptr;
+  unsigned* const nulb = nullptr;
 #define ROW(l) (valid ? o.h[l] + p * kH : nul)
-#define BITS(acc, l) store_bits(acc, o.mb[l] + p * (kH / 32), h, valid && h == 0)
+#define BITS(l) (valid ? o.mb[l] + p * (kH / 32) : nulb)
   fwd_layer<L0, 8, 32, L1, 8>(a, b, pe, blob, prm, lane, h, pf);
-  relu_tiles<8>(a);
-  BITS(a, 0);
-  fwd_layer<L1, 8, 32, L2, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(0));
-  relu_tiles<8>(b);
-  BITS(b, 1);
-  fwd_layer<L2, 8, 32, L3, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(1));
-  relu_tiles<8>(a);
-  BITS(a, 2);
-  fwd_layer<L3, 8, 32, L4, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(2));
-  relu_tiles<8>(b);
-  BITS(b, 3);
-  fwd_layer<L4, 8, 32, L5, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(3));   // skip: [x, pe] (nerf.py:109-110)
-  relu_tiles<8>(a);
-  BITS(a, 4);
-  fwd_layer<L5, 8, 32, L6, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(4));
-  relu_tiles<8>(b);
-  BITS(b, 5);
-  fwd_layer<L6, 8, 32, L7, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(5));
-  relu_tiles<8>(a);
-  BITS(a, 6);
-  fwd_layer<L7, 8, 32, C0, 4>(b, a, pe, blob, prm, lane, h, pf, ROW(6));
-  relu_tiles<8>(b);
-  BITS(b, 7);
-  const float sigma = density_head(b, prm, h);
-  fwd_layer<C0, 4, 16, -1, 0>(a, b, de, blob, prm, lane, h, pf, ROW(7));   // [x, PE4(d)] (nerf.py:117-121)
+  fwd_layer<L1, 8, 32, L2, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(0), BITS(0));
+  fwd_layer<L2, 8, 32, L3, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(1), BITS(1));
+  fwd_layer<L3, 8, 32, L4, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(2), BITS(2));
+  fwd_layer<L4, 8, 32, L5, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(3), BITS(3));   // skip: [x, pe] (nerf.py:109-110)
+  fwd_layer<L5, 8, 32, L6, 8>(b, a, pe, blob, prm, lane, h, pf, ROW(4), BITS(4));
+  fwd_layer<L6, 8, 32, L7, 8>(a, b, pe, blob, prm, lane, h, pf, ROW(5), BITS(5));
+  fwd_layer<L7, 8, 32, C0, 4>(b, a, pe, blob, prm, lane, h, pf, ROW(6), BITS(6));
+  fwd_layer<C0, 4, 16, -1, 0>(a, b, de, blob, prm, lane, h, pf, ROW(7), BITS(7));   // [x, PE4(d)] (nerf.py:117-121)
+  const float sigma = density_head(b, prm, h);    // b: layer 7's outputs, ReLU'd inside C0's pass
 #undef ROW
 #undef BITS
   relu_tiles<4>(a);
