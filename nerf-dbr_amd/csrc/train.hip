@@ -416,51 +416,121 @@ __global__ void train_encode_kernel(const float* __restrict__ rays_o, const floa
 //                  reversed cumsum accumulated in double as torch's CPU cumsum)
 //   g_sigma_i    = g_alpha_i e_i dist_i [sigma_i > 0]                (alpha = 1 - exp(-relu(s) d))
 // then the sigmoid and density-ReLU backward: dpre[p] = (d r, d g, d b, d sigma) pre-activation.
-__global__ void render_train_kernel(const f32x4* __restrict__ rgbs, const float* __restrict__ z, int z_stride,
-                                    const float* __restrict__ rays_d, const float* __restrict__ target, int n_rays,
-                                    int n_samples, float gnorm, float* __restrict__ tbuf, f32x4* __restrict__ dpre,
-                                    float* __restrict__ loss_ray) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rays) return;
+// One wave per ray: lane l holds the contiguous chunk of samples [l c, (l + 1) c), c =
+// ceil(S / 64).  The transmittance product and the backward's reversed cumsum are scans in
+// double over the lanes -- the same products and sums as the sequential restatement,
+// associated differently (~1e-16 relative, far below the floats they are rounded to);
+// rgb_map is summed in sample order, lane after lane.  tbuf holds t_s = float(prod_{i <= s} q_i) for the
+// backward (written and read by the same lane).
+constexpr int kMaxChunk = 16;   // samples per lane at most (1024 per ray)
+__global__ __launch_bounds__(256) void render_train_kernel(const f32x4* __restrict__ rgbs,
+                                                           const float* __restrict__ z, int z_stride,
+                                                           const float* __restrict__ rays_d,
+                                                           const float* __restrict__ target, int n_rays,
+                                                           int n_samples, float gnorm, float* __restrict__ tbuf,
+                                                           f32x4* __restrict__ dpre, float* __restrict__ loss_ray) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n_rays) return;                                   // wave-uniform
   const float dx = rays_d[3L * r], dy = rays_d[3L * r + 1], dz = rays_d[3L * r + 2];
   const float norm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
   const float* zr = z + long(r) * z_stride;
   const long base = long(r) * n_samples;
-  double tacc = 1.0;
-  float rm[3] = {0.0f, 0.0f, 0.0f};
-  for (int s = 0; s < n_samples; ++s) {
-    const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(zr[s + 1], zr[s]) : 1e10f, norm);
-    const f32x4 v = rgbs[base + s];
-    const float e = expf(__fmul_rn(-relu(v[3]), dist));
-    const float alpha = __fsub_rn(1.0f, e);
-    const float T = float(tacc);
-    const float w = __fmul_rn(alpha, T);
+  const int c = (n_samples + 63) / 64;                       // <= kMaxChunk (n_samples <= 1024)
+  const int s0 = min(lane * c, n_samples), s1 = min(s0 + c, n_samples);
+  auto dist_of = [&](int s) { return __fmul_rn(s + 1 < n_samples ? __fsub_rn(zr[s + 1], zr[s]) : 1e10f, norm); };
+  // forward: this lane's product of q, then the exclusive product over the lanes before it
+  double lp = 1.0;
+  for (int s = s0; s < s1; ++s) {
+    const float e = expf(__fmul_rn(-relu(rgbs[base + s][3]), dist_of(s)));
+    lp = __dmul_rn(lp, double(__fadd_rn(__fsub_rn(1.0f, __fsub_rn(1.0f, e)), 1e-10f)));
+  }
+  double incl = lp;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) rm[c] = __fadd_rn(rm[c], __fmul_rn(w, v[c]));
-    tacc = __dmul_rn(tacc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
-    tbuf[base + s] = float(tacc);
+  for (int d = 1; d < 64; d <<= 1) {
+    const double o = __shfl_up(incl, d);
+    if (lane >= d) incl = __dmul_rn(o, incl);
+  }
+  double excl = __shfl_up(incl, 1);
+  if (lane == 0) excl = 1.0;
+  double tacc = excl;
+  float wc[kMaxChunk][3];     // this lane's w_s c_s, in sample order
+#pragma unroll
+  for (int j = 0; j < kMaxChunk; ++j) {
+    const int s = s0 + j;
+    if (s < s1) {
+      const f32x4 v = rgbs[base + s];
+      const float alpha = __fsub_rn(1.0f, expf(__fmul_rn(-relu(v[3]), dist_of(s))));
+      const float w = __fmul_rn(alpha, float(tacc));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) wc[j][k] = __fmul_rn(w, v[k]);
+      tacc = __dmul_rn(tacc, double(__fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f)));
+      tbuf[base + s] = float(tacc);
+    }
+  }
+  // rgb_map = sum_s w_s c_s in sample order (torch's order for this reduction): the running
+  // sum passes from lane to lane, each adding its chunk term by term
+  float rm[3] = {0.0f, 0.0f, 0.0f};
+  const int used = (n_samples + c - 1) / c;                  // lanes holding samples
+  for (int l = 0; l < used; ++l) {
+    if (lane == l)
+#pragma unroll
+      for (int j = 0; j < kMaxChunk; ++j)
+        if (s0 + j < s1)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) rm[k] = __fadd_rn(rm[k], wc[j][k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      rm[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, rm[k]), l));
   }
   float g[3], loss = 0.0f;
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float diff = __fsub_rn(rm[c], target[3L * r + c]);
+  for (int k = 0; k < 3; ++k) {
+    const float diff = __fsub_rn(rm[k], target[3L * r + k]);
     loss = __fadd_rn(loss, __fmul_rn(diff, diff));
-    g[c] = __fmul_rn(gnorm, diff);
+    g[k] = __fmul_rn(gnorm, diff);
   }
-  loss_ray[r] = loss;
-  double suffix = 0.0;     // sum_{i >= s} g_t_i * t_i
-  float g_t = 0.0f;        // g_t_s = g_T_{s+1} (0 for the last sample)
-  for (int s = n_samples - 1; s >= 0; --s) {
-    const float dist = __fmul_rn(s + 1 < n_samples ? __fsub_rn(zr[s + 1], zr[s]) : 1e10f, norm);
+  if (lane == 0) loss_ray[r] = loss;
+  // backward.  g_t_s = g_T_{s+1} = g_w_{s+1} alpha_{s+1} (0 for the last sample): a chunk's
+  // last sample takes it from the next lane's first
+  auto gw_of = [&](const f32x4& v) {
+    return __fadd_rn(__fadd_rn(__fmul_rn(g[0], v[0]), __fmul_rn(g[1], v[1])), __fmul_rn(g[2], v[2]));
+  };
+  float first = 0.0f;
+  if (s0 < s1) {
+    const f32x4 v = rgbs[base + s0];
+    first = __fmul_rn(gw_of(v), __fsub_rn(1.0f, expf(__fmul_rn(-relu(v[3]), dist_of(s0)))));
+  }
+  float next = __shfl_down(first, 1);
+  if (lane == 63) next = 0.0f;
+  // this lane's sum of t_s g_t_s, then the sum over the lanes after it (the reversed cumsum)
+  double ls = 0.0;
+  float nx = next;
+  for (int s = s1 - 1; s >= s0; --s) {
+    const f32x4 v = rgbs[base + s];
+    ls = __dadd_rn(ls, double(__fmul_rn(tbuf[base + s], nx)));
+    nx = __fmul_rn(gw_of(v), __fsub_rn(1.0f, expf(__fmul_rn(-relu(v[3]), dist_of(s)))));
+  }
+  double sinc = ls;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double o = __shfl_down(sinc, d);
+    if (lane + d < 64) sinc = __dadd_rn(sinc, o);
+  }
+  double suffix = __shfl_down(sinc, 1);
+  if (lane == 63) suffix = 0.0;
+  float g_t = next;
+  for (int s = s1 - 1; s >= s0; --s) {
+    const float dist = dist_of(s);
     const f32x4 v = rgbs[base + s];
     const float sg = relu(v[3]);
     const float e = expf(__fmul_rn(-sg, dist));
     const float alpha = __fsub_rn(1.0f, e);
-    const float T = s > 0 ? tbuf[base + s - 1] : 1.0f;
+    const float T = s > s0 ? tbuf[base + s - 1] : float(excl);
     const float t_s = tbuf[base + s];
     const float q = __fadd_rn(__fsub_rn(1.0f, alpha), 1e-10f);
     const float w = __fmul_rn(alpha, T);
-    const float gw = __fadd_rn(__fadd_rn(__fmul_rn(g[0], v[0]), __fmul_rn(g[1], v[1])), __fmul_rn(g[2], v[2]));
+    const float gw = gw_of(v);
     suffix = __dadd_rn(suffix, double(__fmul_rn(t_s, g_t)));
     const float g_q = __fdiv_rn(float(suffix), q);
     const float g_alpha = __fsub_rn(__fmul_rn(gw, T), g_q);
@@ -468,7 +538,7 @@ __global__ void render_train_kernel(const f32x4* __restrict__ rgbs, const float*
     g_t = __fmul_rn(gw, alpha);    // g_T_s = g_t_{s-1}
     f32x4 d;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) d[c] = __fmul_rn(__fmul_rn(__fmul_rn(w, g[c]), __fsub_rn(1.0f, v[c])), v[c]);
+    for (int k = 0; k < 3; ++k) d[k] = __fmul_rn(__fmul_rn(__fmul_rn(w, g[k]), __fsub_rn(1.0f, v[k])), v[k]);
     d[3] = g_sig;
     dpre[base + s] = d;
   }
@@ -1277,7 +1347,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   if ((rc = mark(2)) != NERF_OK) return rc;
   // volume render + loss, their backward (rendering.py:102-143, trainer.py:117-126)
   const float gnorm = float(2.0 / (3.0 * n_total));   // mse_loss backward over the whole step's rays
-  hipLaunchKernelGGL(render_train_kernel, dim3(blocks_for(n_rays, 64)), dim3(64), 0, s, (const f32x4*)a.rgbs, z,
+  hipLaunchKernelGGL(render_train_kernel, dim3(blocks_for(n_rays, 4)), dim3(256), 0, s, (const f32x4*)a.rgbs, z,
                      z_stride, rays_d, target, n_rays, S, gnorm, a.tb, (f32x4*)a.dpre, loss_ray);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks_for(P * (kHeadLd / 4), 256)), dim3(256), 0, s, a.hc,
