@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NERF_ABI_VERSION 2
+#define NERF_ABI_VERSION 3
 
 enum nerf_status {
   NERF_OK = 0,
@@ -286,6 +286,12 @@ enum nerf_train_state { NERF_TR_PARAMS = 0, NERF_TR_GRADS = 1, NERF_TR_EXP_AVG =
 int nerf_trainer_read(nerf_trainer* tr, int what, int net, float* const* host_out, int n_params);
 /* Overwrites one net's gradients (22 host tensors), e.g. to check clip + Adam on given grads. */
 int nerf_trainer_write_grads(nerf_trainer* tr, int net, const float* const* grads, int n_params);
+/* Resuming a run (NeRFTrainer.load_checkpoint, trainer.py:388-399): overwrite one net's state
+ * (what as for nerf_trainer_read; NERF_TR_PARAMS also rewrites the kernels' operand copies)
+ * from host tensors in state-dict order, and set Adam's step count and the current learning
+ * rate (optimizer.state[p]['step'], param_groups[0]['lr']; ExponentialLR's last_epoch = steps). */
+int nerf_trainer_write(nerf_trainer* tr, int what, int net, const float* const* host_in, int n_params);
+int nerf_trainer_set_schedule(nerf_trainer* tr, long steps, double lr);
 /* Clip + Adam + schedule on the gradients as they stand (the update half of train_step). */
 int nerf_trainer_update(nerf_trainer* tr, void* stream);
 /* The learning rate the next update uses (optimizer.param_groups[0]['lr']) and the steps taken. */

@@ -1727,6 +1727,38 @@ int nerf_trainer_write_grads(nerf_trainer* tr, int net, const float* const* grad
   return NERF_OK;
 }
 
+int nerf_trainer_write(nerf_trainer* tr, int what, int net, const float* const* host_in, int n_params) {
+  if (!tr || !host_in) return set_error(NERF_E_INVALID, "nerf_trainer_write: null argument");
+  if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
+  if (n_params != NERF_N_PARAMS) return set_error(NERF_E_INVALID, "expected %d tensors", NERF_N_PARAMS);
+  float* dst = what == NERF_TR_PARAMS ? tr->params : what == NERF_TR_GRADS ? tr->grads
+             : what == NERF_TR_EXP_AVG ? tr->m : what == NERF_TR_EXP_AVG_SQ ? tr->v : nullptr;
+  if (!dst) return set_error(NERF_E_INVALID, "nerf_trainer_write: bad state %d", what);
+  std::vector<float> host(kNetFloats);
+  for (int i = 0; i < NERF_N_PARAMS; ++i) {
+    if (!host_in[i]) return set_error(NERF_E_INVALID, "nerf_trainer_write: null tensor %d", i);
+    std::memcpy(host.data() + param_offset(i), host_in[i], sizeof(float) * param_count(i));
+  }
+  DeviceGuardT dg(tr->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(dst + net * kNetFloats, host.data(), sizeof(float) * kNetFloats, hipMemcpyHostToDevice));
+  if (what == NERF_TR_PARAMS) {   // the kernels' operand copies of the weights
+    hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, 0,
+                       (const float*)tr->params, tr->gemmw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  return NERF_OK;
+}
+
+int nerf_trainer_set_schedule(nerf_trainer* tr, long steps, double lr) {
+  if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  if (steps < 0 || !(lr >= 0.0)) return set_error(NERF_E_INVALID, "nerf_trainer_set_schedule: steps %ld, lr %g", steps, lr);
+  tr->steps = steps;
+  tr->lr = lr;
+  return NERF_OK;
+}
+
 double nerf_trainer_lr(const nerf_trainer* tr) { return tr ? tr->lr : 0.0; }
 long nerf_trainer_steps(const nerf_trainer* tr) { return tr ? tr->steps : 0; }
 double nerf_trainer_gemm_flops(const nerf_trainer* tr) { return tr ? tr->gemm_flops : 0.0; }

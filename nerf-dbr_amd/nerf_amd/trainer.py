@@ -218,6 +218,16 @@ class MI355XTrainer:
         rt._check(self.lib.nerf_trainer_write_grads(self._h, net, ptrs, rt.NERF_N_PARAMS))
         del keep
 
+    def write(self, what: int, net: int, tensors: Mapping[str, np.ndarray]) -> None:
+        """Overwrite one net's parameters / gradients / Adam moments (rt.NERF_TR_*)."""
+        keep, ptrs = rt._param_list(tensors)
+        rt._check(self.lib.nerf_trainer_write(self._h, what, net, ptrs, rt.NERF_N_PARAMS))
+        del keep
+
+    def set_schedule(self, steps: int, lr: float) -> None:
+        """Adam's step count and the current learning rate."""
+        rt._check(self.lib.nerf_trainer_set_schedule(self._h, int(steps), float(lr)))
+
     @property
     def lr(self) -> float:
         """optimizer.param_groups[0]['lr'] for the next step."""
@@ -239,8 +249,84 @@ class MI355XTrainer:
         """Algorithmic fp32 FLOP of the last step's GEMMs."""
         return float(self.lib.nerf_trainer_gemm_flops(self._h))
 
-    def save_checkpoint(self, path: str) -> str:
-        """Reference-format checkpoint (trainer.py:376-384, model entries), loadable by
-        MI355XRenderer.setup."""
+    def _torch_optimizer(self):
+        """torch.optim.Adam + ExponentialLR over CPU stand-ins of the 44 parameters (coarse then
+        fine, state-dict order: NeRFTrainer's `list(coarse.parameters()) + list(fine...)`,
+        trainer.py:54-64) holding this trainer's state, for state_dict() in torch's format."""
+        import torch
+
+        c = self.config
+        params = [torch.nn.Parameter(torch.from_numpy(v.copy()))
+                  for sd in self.state_dicts() for v in sd.values()]
+        opt = torch.optim.Adam(params, lr=float(c["lr"]), weight_decay=float(c["weight_decay"]))
+        sched = torch.optim.lr_scheduler.ExponentialLR(opt, gamma=self._cfg.lr_gamma)
+        steps = self.steps
+        if steps > 0:
+            moments = [(self.exp_avg(n), self.exp_avg_sq(n)) for n in (0, 1)]
+            i = 0
+            for net in (0, 1):
+                for k in self.state_dicts()[net]:
+                    opt.state[params[i]] = {"step": torch.tensor(float(steps)),
+                                            "exp_avg": torch.from_numpy(moments[net][0][k].copy()),
+                                            "exp_avg_sq": torch.from_numpy(moments[net][1][k].copy())}
+                    i += 1
+        opt.param_groups[0]["lr"] = self.lr
+        sched.last_epoch = steps
+        sched._step_count = steps + 1
+        sched._last_lr = [self.lr]
+        return opt, sched
+
+    def save_checkpoint(self, path: str, full: bool = True) -> str:
+        """NeRFTrainer.save_checkpoint (trainer.py:373-386): coarse_model, fine_model, optimizer
+        and scheduler state dicts in torch's format, config and loss histories (a reference
+        NeRFTrainer resumes from it with load_checkpoint); MI355XRenderer.setup reads the model
+        entries.  full=False writes the model entries only."""
         coarse, fine = self.state_dicts()
-        return save_checkpoint(path, coarse, fine)
+        if not full:
+            return save_checkpoint(path, coarse, fine)
+        import os
+
+        import torch
+
+        opt, sched = self._torch_optimizer()
+        ck = {"coarse_model": {k: torch.from_numpy(v) for k, v in coarse.items()},
+              "fine_model": {k: torch.from_numpy(v) for k, v in fine.items()},
+              "optimizer": opt.state_dict(), "scheduler": sched.state_dict(), "config": dict(self.config),
+              "train_losses": list(self.train_losses), "val_losses": list(self.val_losses)}
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        torch.save(ck, path)
+        return path
+
+    def load_checkpoint(self, path: str) -> None:
+        """NeRFTrainer.load_checkpoint (trainer.py:388-399): models, Adam's moments and step,
+        the scheduler's learning rate and the loss histories, from a checkpoint written by the
+        reference trainer or by save_checkpoint (loaded with weights_only=True)."""
+        import torch
+
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        sds = [{k: v.detach().cpu().numpy().astype(np.float32) for k, v in ck[name].items()}
+               for name in ("coarse_model", "fine_model")]
+        for net, sd in enumerate(sds):
+            validate_state_dict(sd)
+            self.write(rt.NERF_TR_PARAMS, net, sd)
+        names = [list(sd.keys()) for sd in sds]
+        opt = ck.get("optimizer")
+        steps, lr = 0, float(self.config["lr"])
+        if opt is not None:
+            state = opt.get("state", {})
+            lr = float(opt["param_groups"][0]["lr"])
+            for which, key in ((rt.NERF_TR_EXP_AVG, "exp_avg"), (rt.NERF_TR_EXP_AVG_SQ, "exp_avg_sq")):
+                for net in (0, 1):
+                    t = {}
+                    for j, k in enumerate(names[net]):
+                        st = state.get(22 * net + j)
+                        t[k] = (st[key].detach().cpu().numpy().astype(np.float32) if st is not None
+                                else np.zeros_like(sds[net][k]))
+                    self.write(which, net, t)
+            steps = max([int(float(st["step"])) for st in state.values()] or [0])
+        sched = ck.get("scheduler")
+        if sched is not None and "_last_lr" in sched:
+            lr = float(sched["_last_lr"][0])
+        self.set_schedule(steps, lr)
+        self.train_losses = list(ck.get("train_losses", []))
+        self.val_losses = list(ck.get("val_losses", []))

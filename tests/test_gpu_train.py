@@ -282,3 +282,52 @@ def test_train_steps_on_two_streams_match_one_stream(fx):
         pa, pb = ref.state_dicts()[net], two.state_dicts()[net]
         for k in T.PARAM_ORDER:
             assert np.array_equal(pa[k], pb[k]), (net, k)
+
+
+def test_train_checkpoint_resume(fx, tmp_path):
+    """save_checkpoint / load_checkpoint (trainer.py:373-399): a trainer resumed from a
+    checkpoint continues exactly as the one that wrote it (bit for bit), and torch's own
+    Adam + ExponentialLR load the checkpoint's optimizer and scheduler state dicts and take
+    the same update (the reference trainer's resume path)."""
+    n = int(fx["n_rays"])
+    a, _ = _trainer(n)
+    for s in range(2):
+        a.train_step(_batch(fx), select_inds=fx[f"step{s}_select"].astype(np.int32), t_rand=fx[f"step{s}_t_rand"])
+    path = a.save_checkpoint(str(tmp_path / "ck.pth"))
+    b, orc = _trainer(n, sd=W.synthetic_models(1))
+    b.load_checkpoint(path)
+    assert b.steps == a.steps == 2 and b.lr == a.lr
+    for net in (0, 1):
+        for get in (lambda t: t.state_dicts()[net], lambda t: t.exp_avg(net), lambda t: t.exp_avg_sq(net)):
+            ga, gb = get(a), get(b)
+            for k in T.PARAM_ORDER:
+                assert np.array_equal(ga[k], gb[k]), (net, k)
+    sel, tr = fx["step2_select"].astype(np.int32), fx["step2_t_rand"]
+    a.train_step(_batch(fx), select_inds=sel, t_rand=tr)
+    b.train_step(_batch(fx), select_inds=sel, t_rand=tr)
+    for net in (0, 1):
+        pa, pb = a.state_dicts()[net], b.state_dicts()[net]
+        for k in T.PARAM_ORDER:
+            assert np.array_equal(pa[k], pb[k]), (net, k)
+    # the reference's resume: torch objects load the state dicts
+    ck = torch.load(path, weights_only=True)
+    with torch.no_grad():
+        for net, name in ((0, "coarse_model"), (1, "fine_model")):
+            for k in T.PARAM_ORDER:
+                orc.nets[net].p[k].copy_(ck[name][k])
+    orc.optimizer.load_state_dict(ck["optimizer"])
+    orc.scheduler.load_state_dict(ck["scheduler"])
+    assert orc.lr == ck["scheduler"]["_last_lr"][0]
+    c, _ = _trainer(n, sd=W.synthetic_models(1))
+    c.load_checkpoint(path)
+    c.train_step(_batch(fx), select_inds=sel, t_rand=tr, update=False)
+    orc.set_grads([c.grads(0), c.grads(1)])
+    orc.clip()
+    orc.update()
+    c.update()
+    assert c.lr == orc.lr and c.steps == 3
+    for net in (0, 1):
+        p_gpu, p_ref = c.state_dicts()[net], orc.params_np(net)
+        for k in T.PARAM_ORDER:
+            d = np.abs(p_gpu[k].astype(np.float64) - p_ref[k])
+            assert np.all(d <= 1e-6 * np.abs(p_ref[k]) + 1e-9), (net, k, d.max())
