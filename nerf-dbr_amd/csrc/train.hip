@@ -632,14 +632,23 @@ __device__ __forceinline__ void fwd_layer(f32x16 (&acc)[8], f32x16 (&prev)[8], c
       const auto sw = __builtin_amdgcn_permlane32_swap(m, m, false, false);
       wbits[t] = unsigned(sw[0]) | unsigned(sw[1]);
     }
-    if (KH > 0 && ug < KH / 4 && prev_row != nullptr) {
-      const int t = ug >> 2, j = ug & 3;
-      *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
-          f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
-      if (ug == KH / 4 - 1 && prev_bits != nullptr && h == 0) {
-        ((u32x4_t*)prev_bits)[0] = u32x4_t{wbits[0], wbits[1], wbits[2], wbits[3]};
-        ((u32x4_t*)prev_bits)[1] = u32x4_t{wbits[4], wbits[5], wbits[6], wbits[7]};
-      }
+    // row piece pc = 4t + j of prev goes out one group late (after group pc + 1's loads), so
+    // that it is younger than the loads the next group waits for: vmcnt retires loads and
+    // stores in issue order, and a store issued before a group's loads made that group wait
+    // for the store's completion too.  A layer without encoding groups stores its last piece
+    // (and the bit words) after its last group's loads.
+    if (KH > 0 && prev_row != nullptr) {
+      auto store_piece = [&](int pc) {
+        const int t = pc >> 2, j = pc & 3;
+        *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
+            f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
+        if (pc == KH / 4 - 1 && prev_bits != nullptr && h == 0) {
+          ((u32x4_t*)prev_bits)[0] = u32x4_t{wbits[0], wbits[1], wbits[2], wbits[3]};
+          ((u32x4_t*)prev_bits)[1] = u32x4_t{wbits[4], wbits[5], wbits[6], wbits[7]};
+        }
+      };
+      if (ug >= 1 && ug - 1 < KH / 4) store_piece(ug - 1);
+      if (ug == G - 1 && G == KH / 4) store_piece(ug);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -745,10 +754,14 @@ __device__ __forceinline__ void bwd_layer(f32x16 (&acc)[8], const f32x16 (&prev)
 #pragma unroll
       for (int o = 0; o < 8; ++o) pf[o] = next_blob[lane + o * 64];
     }
-    if (prev_row != nullptr && ug < 32) {     // 256-wide dZ rows: 32 pieces of 16 B
-      const int t = ug >> 2, j = ug & 3;
-      *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
-          f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
+    if (prev_row != nullptr) {     // 256-wide dZ rows: 32 pieces of 16 B, one group late (fwd_layer)
+      auto store_piece = [&](int pc) {
+        const int t = pc >> 2, j = pc & 3;
+        *(f32x4*)(prev_row + 32 * t + 8 * j + 4 * h) =
+            f32x4{prev[t][4 * j], prev[t][4 * j + 1], prev[t][4 * j + 2], prev[t][4 * j + 3]};
+      };
+      if (ug >= 1 && ug - 1 < 32) store_piece(ug - 1);
+      if (ug == G - 1 && G == 32) store_piece(ug);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
