@@ -94,8 +94,12 @@ class MI355XTrainer:
         self._h = h
         self._loss = torch.zeros(3, dtype=torch.float32, device=self.device)
         self._grad_t = None
+        self._render_dev = None      # inference context for render_image / validate
 
     def close(self) -> None:
+        if getattr(self, "_render_dev", None) is not None:
+            self._render_dev.close()
+            self._render_dev = None
         if getattr(self, "_h", None) is not None and self._h.value:
             if getattr(self, "_grad_t", None) is not None:
                 self.lib.nerf_trainer_set_grad_buffer(self._h, None)   # before the tensor goes
@@ -248,6 +252,80 @@ class MI355XTrainer:
     def gemm_flops(self) -> float:
         """Algorithmic fp32 FLOP of the last step's GEMMs."""
         return float(self.lib.nerf_trainer_gemm_flops(self._h))
+
+    # ------------------------------------------------------------ epochs --
+    def render_image(self, pose, img_shape, focal: float):
+        """NeRFTrainer._render_image (trainer.py:353-371): every pixel's ray through the fine
+        net at n_fine uniform samples (_render_rays' coarse result is discarded there) and
+        volume_render, on the fp32 render path with the trainer's current fine weights (the
+        same rays, z values and compositing as rendering.py); [H, W, 3] device tensor."""
+        import torch
+
+        h, w = int(img_shape[0]), int(img_shape[1])
+        if self._render_dev is None:
+            self._render_dev = rt.Device(self.device_index)
+        self._render_dev.load_weights(rt.NERF_NET_FINE, self.state_dicts()[1])
+        pose = pose.detach().cpu().numpy() if hasattr(pose, "detach") else np.asarray(pose)
+        rgb = torch.empty(h, w, 3, dtype=torch.float32, device=self.device)
+        depth = torch.empty(h, w, dtype=torch.float32, device=self.device)
+        self._render_dev.render(np.asarray(pose, np.float32), w, h, 0, h, float(focal), self.near, self.far,
+                                rt.linspace01(self.n_fine), 0, None, rt.NERF_FP32, rgb, depth,
+                                stream=torch.cuda.current_stream(self.device))
+        return rgb
+
+    def validate(self, val_dataset) -> float:
+        """NeRFTrainer.validate (trainer.py:140-170): mean MSE of the rendered image over the
+        first five validation views."""
+        import torch
+
+        losses = []
+        for i in range(min(5, len(val_dataset))):
+            batch = val_dataset[i]
+            image = torch.as_tensor(np.asarray(batch["image"].detach().cpu() if hasattr(batch["image"], "detach")
+                                               else batch["image"], np.float32)).to(self.device)
+            pred = self.render_image(batch["pose"], tuple(image.shape[:2]), float(batch["focal"]))
+            losses.append(float(torch.mean((pred - image) ** 2).item()))
+        return float(np.mean(losses))
+
+    def train(self, train_dataset, val_dataset=None, n_epochs: int = 100, checkpoint_dir: str = "checkpoints"):
+        """NeRFTrainer.train (trainer.py:172-244): resume from the latest
+        checkpoint_epoch_<n>.pth in checkpoint_dir, then per epoch one train_step per image, the
+        epoch's mean loss appended to train_losses, validate every 10th epoch, a checkpoint every
+        checkpoint_frequency epochs."""
+        import glob
+        import os
+        import re
+
+        start = 0
+        found = []
+        for f in glob.glob(os.path.join(checkpoint_dir, "checkpoint_epoch_*.pth")):
+            m = re.search(r"checkpoint_epoch_(\d+)\.pth$", f)
+            if m:
+                found.append((int(m.group(1)), f))
+        if found:
+            latest = max(found)[1]
+            print(f"Found checkpoint: {latest}")
+            self.load_checkpoint(latest)
+            start = len(self.train_losses)
+            print(f"Resuming training from epoch {start + 1}/{n_epochs}")
+        else:
+            print(f"No checkpoint found. Starting training from epoch 1/{n_epochs}")
+        if start >= n_epochs:
+            print(f"Training already completed! ({start}/{n_epochs} epochs)")
+            return
+        for epoch in range(start, n_epochs):
+            losses = [self.train_step(train_dataset[i]) for i in range(len(train_dataset))]
+            avg = float(np.mean(losses))
+            self.train_losses.append(avg)
+            if val_dataset is not None and (epoch + 1) % 10 == 0:
+                val = self.validate(val_dataset)
+                self.val_losses.append(val)
+                print(f"Epoch {epoch + 1}: Train Loss = {avg:.4f}, Val Loss = {val:.4f}")
+            else:
+                print(f"Epoch {epoch + 1}: Train Loss = {avg:.4f}")
+            if self.checkpoint_frequency and (epoch + 1) % int(self.checkpoint_frequency) == 0:
+                self.save_checkpoint(os.path.join(checkpoint_dir, f"checkpoint_epoch_{epoch + 1}.pth"))
+        print("Training completed!")
 
     def _torch_optimizer(self):
         """torch.optim.Adam + ExponentialLR over CPU stand-ins of the 44 parameters (coarse then

@@ -331,3 +331,58 @@ def test_train_checkpoint_resume(fx, tmp_path):
         for k in T.PARAM_ORDER:
             d = np.abs(p_gpu[k].astype(np.float64) - p_ref[k])
             assert np.all(d <= 1e-6 * np.abs(p_ref[k]) + 1e-9), (net, k, d.max())
+
+
+class _Views:
+    """A dataset of (image, pose, focal) batches as SyntheticDataset.__getitem__ returns them
+    (loader.py:71-76), random targets."""
+
+    def __init__(self, n, h, w, seed):
+        rng = np.random.RandomState(seed)
+        self.items = [{"image": torch.from_numpy(rng.rand(h, w, 3).astype(np.float32)),
+                       "pose": torch.from_numpy(_look_at([3.0 * np.cos(a), 3.0 * np.sin(a), 1.5])),
+                       "focal": 0.9 * w} for a in np.linspace(0.0, 1.0, n)]
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        return self.items[i]
+
+
+def test_train_render_image_matches_oracle():
+    """NeRFTrainer._render_image (trainer.py:353-371): fine net, n_fine uniform samples,
+    rendering.py's volume_render, against the oracle's restatement at the fp32 gate."""
+    from oracle import nerf_oracle as O
+
+    gpu, orc = _trainer(64, {"n_fine": 48})
+    h, w = 12, 16
+    pose = _look_at([2.2, -2.9, 1.4])
+    rgb = gpu.render_image(torch.from_numpy(pose), (h, w), 14.0).cpu().numpy()
+    ro, rd = T.trainer_rays(pose, h, w, 14.0)
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    z = O.uniform_z(48).expand(ro.shape[0], 48)
+    with torch.no_grad():
+        ref = orc._render(orc.nets[1], ro, rd, z).reshape(h, w, 3).numpy()
+    err = float(np.abs(rgb - ref).max())
+    print(f"\n[train] render_image vs oracle: rgb max-abs {err:.2e}")
+    assert err < 1e-4
+
+
+def test_train_epoch_loop_checkpoints_and_resume(tmp_path):
+    """NeRFTrainer.train (trainer.py:172-244): epochs of train_step over the dataset, the
+    mean loss per epoch, validation every 10th epoch, checkpoint_epoch_<n>.pth every
+    checkpoint_frequency epochs, and a second run resuming from the latest of them."""
+    data, val = _Views(3, 10, 12, 1), _Views(2, 10, 12, 2)
+    cfg = {"checkpoint_frequency": 2}
+    a, _ = _trainer(32, cfg)
+    a.train(data, val, n_epochs=3, checkpoint_dir=str(tmp_path))
+    assert len(a.train_losses) == 3 and a.steps == 9
+    assert (tmp_path / "checkpoint_epoch_2.pth").exists() and not (tmp_path / "checkpoint_epoch_3.pth").exists()
+    b, _ = _trainer(32, cfg)
+    b.train(data, val, n_epochs=4, checkpoint_dir=str(tmp_path))     # resumes after epoch 2
+    assert len(b.train_losses) == 4 and b.steps == 12
+    assert b.train_losses[:2] == a.train_losses[:2]
+    assert (tmp_path / "checkpoint_epoch_4.pth").exists()
+    v = b.validate(val)
+    assert np.isfinite(v) and v > 0.0
