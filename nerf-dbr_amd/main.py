@@ -4,10 +4,13 @@
 
 Same flags (``--data_dir --epochs --skip_training --checkpoint --benchmark_only``,
 ``main.py:202-217``) and the same default grid (200x150 / 400x300 / 800x600 x 32 / 64 /
-128 spp, 2 views, ``main.py:134-141``).  Training is outside this package's scope:
-without ``--benchmark_only``/``--skip_training`` it stops with a message, like the
-reference does when its dataset is missing.  ``--synthetic-checkpoint`` writes the
-deterministic conditioned checkpoint (nerf_amd.weights) first.
+128 spp, 2 views, ``main.py:134-141``).  Without ``--benchmark_only``/``--skip_training``
+it trains first, as ``train_nerf`` does (``main.py:65-109``), with ``MI355XTrainer`` and
+main.py's configuration; the dataset comes from the reference's own loader
+(``src.data.loader.load_synthetic_data``, importable when run from the reference checkout:
+the loader is not part of this package), and without it the CLI stops with a message.
+``--synthetic-checkpoint`` writes the deterministic conditioned checkpoint
+(nerf_amd.weights) first.
 """
 from __future__ import annotations
 
@@ -39,9 +42,21 @@ def main(argv=None) -> int:
     from nerf_amd.benchmark.benchmark_suite import UnifiedBenchmarkSuite
 
     if not (args.skip_training or args.benchmark_only):
-        print("Training is not part of this package (the render path is); run with --benchmark_only "
-              "and a reference-format checkpoint.")
-        return 1
+        try:
+            from src.data.loader import load_synthetic_data   # the reference's loader (its checkout on the path)
+        except ImportError:
+            print("Training needs the reference's dataset loader (src/data/loader.py): run from the reference "
+                  "checkout, or use --benchmark_only with a reference-format checkpoint.")
+            return 1
+        from nerf_amd.trainer import MAIN_CONFIG, MI355XTrainer
+
+        datasets = load_synthetic_data(args.data_dir, "cpu")
+        if "train" not in datasets:
+            raise ValueError(f"Training dataset not found in {args.data_dir}")
+        trainer = MI355XTrainer(dict(MAIN_CONFIG))
+        trainer.train(datasets["train"], datasets.get("val"), args.epochs)
+        trainer.save_checkpoint(args.checkpoint)
+        print(f"\nTraining completed! Model saved to: {args.checkpoint}")
     if args.synthetic_checkpoint:
         W.write_synthetic_checkpoint(args.checkpoint)
     if not os.path.exists(args.checkpoint):

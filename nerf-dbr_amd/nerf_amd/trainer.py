@@ -40,6 +40,26 @@ DEFAULTS = {
 }
 
 
+# main.py:get_default_config (main.py:25-61), less the device key
+MAIN_CONFIG = {
+    "lr": 3e-4,
+    "lr_decay": 0.1,
+    "decay_steps": 250000,
+    "n_rays": 2048,
+    "n_coarse": 64,
+    "n_fine": 128,
+    "hidden_dim": 256,
+    "position_encoding_levels": 10,
+    "direction_encoding_levels": 4,
+    "chunk_size": 1024,
+    "near": 2.0,
+    "far": 6.0,
+    "gradient_clipping": 1.0,
+    "weight_decay": 1e-6,
+    "checkpoint_frequency": 25,
+}
+
+
 def _shapes():
     out = []
     for name, o, i in LAYER_SPECS:
