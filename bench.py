@@ -271,7 +271,8 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
     flop = tr.gemm_flops()
     out = {"workload": "NeRFTrainer.train_step, main.py config: 2048 rays of a 400x400 target, 64 stratified "
                        "coarse + 128 uniform fine samples, both nets forward+backward, clip 1.0, Adam, ExponentialLR",
-           "dtype": "fp32", "steps": n_steps, "n_gpus": world, "ms_per_step": 1e3 * dt, "steps_per_s": 1.0 / dt,
+           "dtype": "fp32 (weight-gradient GEMMs: split bf16, 3 bf16 MFMAs per fp32 product, fp32 accumulate)",
+           "steps": n_steps, "n_gpus": world, "ms_per_step": 1e3 * dt, "steps_per_s": 1.0 / dt,
            "rays_per_s": TRAIN_RAYS / dt, "stage_ms_rank0": st,
            "parallelism": "1 GPU" if world == 1 else f"data parallel x{world}: 2048/{world} rays per rank + "
                                                      f"{'RCCL' if torch.distributed.get_backend() == 'nccl' else 'gloo'} "
@@ -281,7 +282,9 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
                     "frac": flop / (gemm_ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"],
                     "note": "all forward, backward-data and weight-gradient GEMMs of both nets (unpadded "
                             "MACs x 2) over the forward_gemm + backward_gemm stages (HIP events of profiled "
-                            "steps, the two nets' passes one after the other)"},
+                            "steps, the two nets' passes one after the other), against the fp32 MFMA peak; "
+                            "the weight gradients run on the bf16 MFMA (split bf16) and are bound by HBM, "
+                            "so this is an fp32-equivalent rate (DESIGN.md section 10)"},
            "loss_first_last": [losses[0], losses[-1]]}
     tr.close()
     if cpu_seconds > 0 and rank == 0 and world == 1:

@@ -108,18 +108,30 @@ constexpr long kGemmFloats = kBwdBlob + round_up(int(bwd_layer_offset(kBwdLayers
 // Per-sample activation workspace (floats per sample; each array [P][ld])
 constexpr int kPeLd = 64, kDpeLd = 28;
 
-// weight-gradient k tiles: 16 sample rows (one LDS-DMA buffer of 26-37 KiB, three in flight)
-constexpr int BK = 16;
+// weight-gradient k tiles: 16 sample rows (one LDS-DMA buffer of 26-37 KiB, four in flight)
+#ifndef NERF_WG_BK
+#define NERF_WG_BK 16
+#endif
+constexpr int BK = NERF_WG_BK;
+#ifndef NERF_WG_BUFS
+#define NERF_WG_BUFS 4
+#endif
+constexpr int kWBufs = BK == 16 ? NERF_WG_BUFS : 2;   // LDS-DMA buffers in flight (LDS budget)
+#ifndef NERF_WGRAD_X3
+#define NERF_WGRAD_X3 1
+#endif
+constexpr bool kWgradX3 = NERF_WGRAD_X3;   // split-bf16 weight gradients (wgrad_tile_x3); 0: fp32 MFMA
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------- weight gradients --
 // Partial weight gradients dW[m][n] = sum_k dZ[k][m] X[k][n] over one split of the samples
-// (k), on v_mfma_f32_32x32x2_f32.  One workgroup tile covers the whole [M][N] gradient
+// (k), on the split-bf16 MFMA (wgrad_tile_x3; NERF_WGRAD_X3=0: v_mfma_f32_32x32x2_f32,
+// wgrad_tile).  One workgroup tile covers the whole [M][N] gradient
 // (256 x 256 over 8 waves of 64 x 128 for the 256-wide layers; wgrad_shape), so both
 // operands are read once.  k tiles of BK sample rows move HBM -> LDS by LDS-DMA
-// (global_load_lds_dwordx4: 1 KiB per wave instruction, no registers, no VALU), three
-// buffers deep and issued two tiles ahead: each wave waits for its own pieces with a
+// (global_load_lds_dwordx4: 1 KiB per wave instruction, no registers, no VALU), kWBufs
+// buffers deep and issued kWBufs - 1 tiles ahead: each wave waits for its own pieces with a
 // counted vmcnt, and one barrier per k tile publishes the tile and frees the buffer of the
 // tile before.  The first column tile's waves also sum dZ over k for their rows (the bias
 // gradient).
@@ -162,7 +174,8 @@ struct WGeo {
   static constexpr int kInsPerWave = (kIns + WAVES - 1) / WAVES;
   static constexpr int kOffB1 = BK * BMT * 4, kOffB2 = kOffB1 + BK * W1 * 4;
   static constexpr int kBufBytes = round_up(kOffB2 + BK * W2 * 4 + 128, 1024);   // B2's last tile reads past W2
-  static constexpr int kBufs = 3;
+  static constexpr int kBufs = kWBufs;
+  static_assert(kBufs >= 2 && kBufs <= 4, "pipeline depth");
   static_assert(kWM * kWN == WAVES && kTN1 * 32 * kWN == W1, "tile geometry");
   static_assert(BK * kR16A % 64 == 0 && BK * kR16B1 % 64 == 0, "whole DMA instructions");
   static_assert(kBufs * kBufBytes <= 160 * 1024, "LDS budget");
@@ -231,6 +244,62 @@ __device__ __forceinline__ void wgrad_tile(const float* __restrict__ buf, f32x16
   }
 }
 
+// The same k tile on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, one MFMA per 16 sample rows):
+// each fp32 operand v is split into v_hi = bf16(v) and v_lo = bf16(v - v_hi) as it is read
+// from LDS, and each product is A_hi.B_hi + A_hi.B_lo + A_lo.B_hi (mlp_bf16x3.hip's scheme;
+// the dropped A_lo.B_lo is ~2^-16 relative), accumulated in fp32.  Per product the error is
+// ~2^-17 relative; over a gradient's k ~ 1e5 samples it stays below the fp32 summation-order
+// differences already present (those grow as sqrt(k), this does not).  Lane l holds rows
+// k = 8 (l / 32) + q, q < 8, of its A row / B column, so BK = 16 is one MFMA k step.
+typedef __bf16 wg_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void wg_split8(const float (&v)[8], u32x4_t& hi, u32x4_t& lo) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const float a = v[2 * d], b = v[2 * d + 1];
+    const unsigned h2 = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, wg_bf16x2));
+    const float ha = __builtin_bit_cast(float, h2 << 16), hb = __builtin_bit_cast(float, h2 & 0xFFFF0000u);
+    hi[d] = h2;
+    lo[d] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{__fsub_rn(a, ha), __fsub_rn(b, hb)}, wg_bf16x2));
+  }
+}
+template <class G, int BMT, int W1, int W2>
+__device__ __forceinline__ void wgrad_tile_x3(const float* __restrict__ buf, f32x16 (&acc)[2][G::kTN], float& bsum,
+                                              int wm, int wn, int h, int l32, int t) {
+  static_assert(BK == 16, "one bf16 MFMA k step per k tile");
+  const float* as = buf + 8 * h * BMT + wm * 64 + l32;
+  const float* b1 = buf + G::kOffB1 / 4 + 8 * h * W1 + 32 * G::kTN1 * wn + l32;
+  const float* b2 = buf + G::kOffB2 / 4 + 8 * h * W2 + 32 * wn + l32;
+  u32x4_t ahi[2], alo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = as[q * BMT + 32 * i];
+    wg_split8(v, ahi[i], alo[i]);
+  }
+#pragma unroll
+  for (int j = 0; j < G::kTN; ++j) {
+    if (j >= G::kTN1 && wtile_col<G, W1>(wn, j) >= W1 + W2) continue;   // wave-uniform: no such tile
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = j < G::kTN1 ? b1[q * W1 + 32 * j] : b2[q * W2 + 32 * G::kWN * (j - G::kTN1)];
+    u32x4_t bhi, blo;
+    wg_split8(v, bhi, blo);
+    const bf16x8 bh = __builtin_bit_cast(bf16x8, bhi), bl = __builtin_bit_cast(bf16x8, blo);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16x8 ah = __builtin_bit_cast(bf16x8, ahi[i]), al = __builtin_bit_cast(bf16x8, alo[i]);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i][j], 0, 0, 0);
+    }
+  }
+  if (t < BMT) {
+#pragma unroll
+    for (int kr = 0; kr < BK; ++kr) bsum = __fadd_rn(bsum, buf[kr * BMT + t]);
+  }
+}
+
 // One split (k range) of one job: the workgroup's whole M x N partial.
 // An opaque SGPR copy: the job's arguments come from a dynamically indexed kernel-argument
 // table, and without this the compiler re-loads them per use inside the k loop (each
@@ -263,21 +332,24 @@ __device__ __forceinline__ void wgrad_split(GemmArgs g, int split, float* lds) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   float bsum = 0.0f;
-  // tiles 0 and 1 in flight; iteration it: own pieces of tile it landed (tile it+1's
-  // may still be in flight), barrier (tile it published, buffer of tile it-1 free),
-  // tile it+2 into that buffer, then tile it from LDS
+  // tiles 0 .. kBufs-2 in flight; iteration it: own pieces of tile it landed (younger
+  // tiles' may still be in flight), barrier (tile it published, buffer of tile it-1 free),
+  // tile it+kBufs-1 into that buffer, then tile it from LDS
   if (nt > 0) issue_ktile<G>(g, kbeg, kend, lds0, w, lane);
-  if (nt > 1) issue_ktile<G>(g, kbeg + BK, kend, lds0 + G::kBufBytes, w, lane);
+#pragma unroll
+  for (int p = 1; p < G::kBufs - 1; ++p)
+    if (p < nt) issue_ktile<G>(g, kbeg + p * BK, kend, lds0 + unsigned(p * G::kBufBytes), w, lane);
   int buf = 0;
   for (int it = 0; it < nt; ++it) {
-    if (it + 1 < nt) wait_vmcnt(G::kInsPerWave);
+    if (G::kBufs == 4 && it + 2 < nt) wait_vmcnt(2 * G::kInsPerWave);   // younger tiles may stay in flight
+    else if (G::kBufs >= 3 && it + 1 < nt) wait_vmcnt(G::kInsPerWave);
     else wait_vmcnt(0);
     compiler_fence();
     __builtin_amdgcn_s_barrier();
     compiler_fence();
-    if (it + 2 < nt) {
-      const int b2 = buf >= 1 ? buf - 1 : G::kBufs - 1;      // (it + 2) % 3
-      issue_ktile<G>(g, kbeg + (it + 2) * BK, kend, lds0 + unsigned(b2 * G::kBufBytes), w, lane);
+    if (it + G::kBufs - 1 < nt) {
+      const int nb = buf >= 1 ? buf - 1 : G::kBufs - 1;      // (it + kBufs - 1) % kBufs
+      issue_ktile<G>(g, kbeg + (it + G::kBufs - 1) * BK, kend, lds0 + unsigned(nb * G::kBufBytes), w, lane);
     }
     float* cur = lds + buf * (G::kBufBytes / 4);
     const int valid = kend - (kbeg + it * BK);
@@ -286,7 +358,8 @@ __device__ __forceinline__ void wgrad_split(GemmArgs g, int split, float* lds) {
         if (i / BMT >= valid) cur[i] = 0.0f;
       __syncthreads();
     }
-    wgrad_tile<G, BMT, W1, W2>(cur, acc, bsum, wm, wn, h, l32, t);
+    if constexpr (kWgradX3) wgrad_tile_x3<G, BMT, W1, W2>(cur, acc, bsum, wm, wn, h, l32, t);
+    else wgrad_tile<G, BMT, W1, W2>(cur, acc, bsum, wm, wn, h, l32, t);
     buf = buf + 1 == G::kBufs ? 0 : buf + 1;
   }
   float* c = g.c + long(split) * g.c_split;
@@ -369,7 +442,7 @@ __global__ void train_rays_kernel(Pose pose, int width, int n_pix, float half_w,
 
 // Sample points o + d*z and their encodings (nerf.py:24-45): pe [P][64] =
 // [x, sin/cos(2^k pi x) k < 10, 0], dpe [P][28] = [d, sin/cos(2^k pi d) k < 4, 0].
-__global__ void train_encode_kernel(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+__global__ __launch_bounds__(256) void train_encode_kernel(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
                                     const float* __restrict__ z, int z_stride, int n_samples, long n_points,
                                     float* __restrict__ pe, float* __restrict__ dpe) {
   const long p = long(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1267,13 +1340,19 @@ WJob plan_wjob(int M, int N, long P, int want, size_t& cursor) {
 }
 
 // Workgroups per weight-gradient job of a net, one per CU in all: in proportion to the
-// job's time per sample, measured on MI355X with each job alone on the chip (rocprofv3,
-// main.py's config; relative to a 256 x 256 layer): 256 x 319 1.30, 256 x 63 0.34,
-// 128 x 283 0.74 (its column tiles do not split evenly over the SIMDs).
+// job's time per sample relative to a 256 x 256 layer.  On the split-bf16 MFMA the jobs are
+// close to HBM-bound, so the weights sit near their operand bytes per sample (256 x 319
+// 1.125, 256 x 63 0.625, 128 x 283 0.80); the values were tuned on MI355X from there
+// (tools/train_lab.py, whole-step wall time).  On the fp32 MFMA they were the MFMA times:
+// 1.30, 0.34, 0.74.
 void wgrad_splits(int (&want)[kMaxWJobs]) {
   double w[kMaxWJobs], total = 0.0;
-  for (int l = 0; l < 8; ++l) w[l] = l == 0 ? 0.34 : l == 4 ? 1.30 : 1.0;
-  w[8] = 0.74;
+#ifndef NERF_WG_COST
+#define NERF_WG_COST 0.52, 1.16, 0.78
+#endif
+  const double c[3] = {NERF_WG_COST};
+  for (int l = 0; l < 8; ++l) w[l] = l == 0 ? c[0] : l == 4 ? c[1] : 1.0;
+  w[8] = c[2];
   for (double x : w) total += x;
   const int cus = current_device_cus();
   int sum = 0;
