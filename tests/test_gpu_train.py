@@ -2,11 +2,14 @@
 oracle's restatement of NeRFTrainer.train_step (oracle/nerf_train_oracle.py),
 itself pinned bit-exactly to the reference trainer (tests/test_train_oracle.py).
 
-Tolerances (fp32 everywhere; the GPU's GEMMs are exact fp32 fma chains in another
-summation order than oneDNN's, so the two differ at fp32 rounding level):
+Tolerances (fp32 data; the forward and backward-data GEMMs are exact fp32 fma chains in
+another summation order than oneDNN's, the weight-gradient GEMMs split each fp32 operand
+into two bf16 parts and sum three bf16 products per fp32 product in fp32, ~2^-17 relative
+per product):
   * loss: relative 1e-5;
-  * gradients: measured (tools/train_diag.py) at 1.5e-7 - 4e-7 normwise relative for
-    every tensor of a net until a ReLU flips in the backward pass: a pre-activation within
+  * gradients: measured (tools/train_diag.py) at 1e-7 - 2.6e-6 normwise relative for
+    every tensor of a net (1.5e-7 - 4e-7 with fp32 weight-gradient GEMMs) until a ReLU
+    flips in the backward pass: a pre-activation within
     rounding of 0 is positive in one run and not in the other, which moves that sample's
     gradient below the flip by a whole term (one of 32,768 samples: ~3e-5 on the layer's
     bias sum, 1e-4 - 3.7e-4 on the layers under it).  fp32 itself does this: the oracle
@@ -15,7 +18,9 @@ summation order than oneDNN's, so the two differ at fp32 rounding level):
     everywhere else.  A flip in the forward pass moves an activation by ~1e-7 only.  So:
     every tensor normwise <= 1e-3 and every element within 2e-3 * max|g_ref|; the heads
     with no hidden ReLU between them and the loss (color_layers.1, density_head)
-    normwise <= 1e-5;
+    normwise <= 1e-5; the fixture step's coarse net, where no ReLU flips, every tensor
+    normwise <= 2e-5 (pins the split-bf16 weight gradients: a dropped hi*lo term would
+    be ~2e-3);
   * clip + Adam + schedule on the GPU's own gradients vs torch.optim.Adam on the same
     gradients: parameters within 1e-6 relative + 1e-9 absolute, lr bit-equal; the clipped
     gradients within 1e-5 relative (torch's clip norm accumulates in fp32, ours in fp64).
@@ -90,6 +95,8 @@ def test_train_step_grads_match_oracle(fx):
     assert abs(loss - ref[0]) <= 1e-5 * abs(ref[0]), (loss, ref[0])
     assert abs(loss - float(fx["step0_loss"])) <= 1e-5 * abs(ref[0])    # the reference's own loss
     worst, med = _check_step_grads(gpu, orc, "fixture")
+    coarse = _compare_grads(gpu.grads(0), orc.grads(0), ("fixture", 0))
+    assert max(coarse) <= 2e-5, dict(zip(T.PARAM_ORDER, coarse))   # no flips in this net's step
     print(f"\n[train] loss gpu {loss:.9g} oracle {ref[0]:.9g}; grad rel err worst {worst:.3g} median {med:.3g}")
 
 
