@@ -267,6 +267,29 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
     tr.set_profiling(False)
     losses.append(float(step(4 + n_steps)[0].item()))
     st = {k: float(np.mean([s[k] for s in stages])) for k in stages[0]}
+    # the same step with the forward on the split-bf16 MFMA (precision "bf16x3"), from the
+    # parameters as they now stand
+    tr.set_precision("bf16x3")
+    for i in range(2):
+        step(5 + n_steps + i)
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    for i in range(n_steps):
+        step(7 + n_steps + i)
+    sync_barrier(world)
+    dt_x3 = D.reduce_max(time.perf_counter() - t0) / n_steps
+    tr.set_profiling(True)
+    stages_x3 = []
+    for i in range(2):
+        step(7 + 2 * n_steps + i)
+        stages_x3.append(tr.stage_ms())
+    tr.set_profiling(False)
+    tr.set_precision("fp32")
+    x3 = {"ms_per_step": 1e3 * dt_x3, "rays_per_s": TRAIN_RAYS / dt_x3,
+          "stage_ms_rank0": {k: float(np.mean([s[k] for s in stages_x3])) for k in stages_x3[0]},
+          "note": "precision 'bf16x3': the forward on the split-bf16 MFMA (mlp_bf16x3.hip's kernel with the "
+                  "rows and ReLU bits the backward reads); gradients as close to the float64 step as the "
+                  "reference's fp32 step (tests/test_gpu_train.py); the default line above is fp32"}
     gemm_ms = st["forward_gemm"] + st["backward_gemm"]
     flop = tr.gemm_flops()
     out = {"workload": "NeRFTrainer.train_step, main.py config: 2048 rays of a 400x400 target, 64 stratified "
@@ -285,7 +308,7 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
                             "steps, the two nets' passes one after the other), against the fp32 MFMA peak; "
                             "the weight gradients run on the bf16 MFMA (split bf16) and are bound by HBM, "
                             "so this is an fp32-equivalent rate (DESIGN.md section 10)"},
-           "loss_first_last": [losses[0], losses[-1]]}
+           "loss_first_last": [losses[0], losses[-1]], "bf16x3_forward": x3}
     tr.close()
     if cpu_seconds > 0 and rank == 0 and world == 1:
         # the oracle's step (PyTorch-CPU autograd restatement of NeRFTrainer.train_step)

@@ -209,11 +209,43 @@ __device__ __forceinline__ f32x16 mfma3(const bf16x8& ahi, const bf16x8& alo, co
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc, 0, 0, 0);
 }
 
+// Training outputs (launch_mlp_bf16x3_train): as each accumulator tile is converted, its
+// ReLU'd fp32 values also go out as the sample's row (one 16-B piece per two dwords:
+// registers 4j..4j+3 are features 32t + 8j + 4h + 0..3) and, for trunk layers, its ReLU bits
+// as one word per tile (bit acc_row(r, h) of register r), both halves merged by a lane swap.
+struct TrainSink {
+  X3TrainOut o;
+  long p;
+  bool valid;
+  unsigned bits[2];
+};
+template <bool kTrain>
+__device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot, const f32x16& tile, int pr, int h) {
+  if constexpr (kTrain) {
+    if (l < 8) {
+      const unsigned m = (tile[2 * pr] > 0.0f ? 1u : 0u) << acc_row(2 * pr, h) |
+                         (tile[2 * pr + 1] > 0.0f ? 1u : 0u) << acc_row(2 * pr + 1, h);
+      sk.bits[slot] = (pr == 0 ? 0u : sk.bits[slot]) | m;
+      if (pr == 7) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(sk.bits[slot], sk.bits[slot], false, false);
+        if (sk.valid && h == 0) sk.o.mb[l][sk.p * 8 + t] = unsigned(sw[0]) | unsigned(sw[1]);
+      }
+    }
+    if (pr & 1) {
+      const int j = pr >> 1;
+      float* row = l < 8 ? sk.o.h[l] + sk.p * 256 : sk.o.hc + sk.p * 132;
+      if (sk.valid)
+        *(f32x4*)(row + 32 * t + 8 * j + 4 * h) =
+            f32x4{relu(tile[4 * j]), relu(tile[4 * j + 1]), relu(tile[4 * j + 2]), relu(tile[4 * j + 3])};
+    }
+  }
+}
+
 // One layer: reads the previous layer's fragments (ih/il), fills the next's (oh/ol).
-template <int L>
+template <int L, bool kTrain>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
                                          u32x4 (&ol)[16], bf16x8 (&ra)[kRing][4], bf16x8 (&rb)[kRing][2],
-                                         const Ctx& cx) {
+                                         const Ctx& cx, TrainSink& sk) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
   constexpr int KU = ksteps_bf16(L);
@@ -239,19 +271,24 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
-        if (kConvert && q == 0 && u == dword_unit_in(m))
+        if (kConvert && q == 0 && u == dword_unit_in(m)) {
           convert_dword(acc[6 + t], pr, ih[2 * (6 + t) + (pr >> 2)], il[2 * (6 + t) + (pr >> 2)]);
-        if (q >= 1 && u == dword_unit_out(KU, m))
+          sink_dword<kTrain>(sk, L > 0 ? L - 1 : 0, 6 + t, t, acc[6 + t], pr, cx.h);
+        }
+        if (q >= 1 && u == dword_unit_out(KU, m)) {
           convert_dword(acc[2 * q - 2 + t], pr, oh[2 * (2 * q - 2 + t) + (pr >> 2)], ol[2 * (2 * q - 2 + t) + (pr >> 2)]);
+          sink_dword<kTrain>(sk, L, 2 * q - 2 + t, t, acc[2 * q - 2 + t], pr, cx.h);
+        }
       }
     }
   }
 }
 
-template <bool kExplicit>
+template <bool kExplicit, bool kTrain>
 __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __restrict__ blob,
                                                                  const float* __restrict__ prm_g, SampleSrc src,
-                                                                 long n_points, f32x4* __restrict__ out) {
+                                                                 long n_points, f32x4* __restrict__ out,
+                                                                 X3TrainOut tro) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -275,6 +312,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
     const long p0 = (tile * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
     Ctx cx = cx0;
     asm volatile("" : "+s"(cx.blob));   // keep the 132 chunk addresses out of SGPRs across tiles
+    TrainSink sk{tro, p0, p0 < n_points, {0u, 0u}};
     {
       float x[3], d[3], pef[32], def[16];
       fetch_sample<kExplicit>(src, p0 < n_points ? p0 : n_points - 1, x, d);
@@ -300,22 +338,22 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
     wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
     stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
-    if (res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
+    if (!kTrain && res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
     bf16x8 ra[kRing][4], rb[kRing][2];
     f32x16 acc[8];
 #pragma unroll
     for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
 
     u32x4 aH[16], aL[16], bH[16], bL[16];
-    layer_x3<L0>(acc, bH, bL, aH, aL, ra, rb, cx);
-    layer_x3<L1>(acc, aH, aL, bH, bL, ra, rb, cx);
-    layer_x3<L2>(acc, bH, bL, aH, aL, ra, rb, cx);
-    layer_x3<L3>(acc, aH, aL, bH, bL, ra, rb, cx);
-    layer_x3<L4>(acc, bH, bL, aH, aL, ra, rb, cx);   // skip: [x, pe] (nerf.py:109-110)
-    layer_x3<L5>(acc, aH, aL, bH, bL, ra, rb, cx);
-    layer_x3<L6>(acc, bH, bL, aH, aL, ra, rb, cx);
-    layer_x3<L7>(acc, aH, aL, bH, bL, ra, rb, cx);
-    layer_x3<C0>(acc, bH, bL, aH, aL, ra, rb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+    layer_x3<L0, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
+    layer_x3<L1, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<L2, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
+    layer_x3<L3, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<L4, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // skip: [x, pe] (nerf.py:109-110)
+    layer_x3<L5, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<L6, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
+    layer_x3<L7, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<C0, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // [x, PE4(d)] (nerf.py:117-121)
 
     // Heads (nerf.py:114, 123-129): one tile, density row 3 over L7's fragments
     // (bH/bL, C0's input, k-steps 0..15), colour rows 0-2 over C0's output
@@ -344,13 +382,23 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
 #pragma unroll
       for (int m = 0; m < 16; ++m)
         if (i < 8 && m / 2 == i)
+          {
           convert_dword(acc[2 + (m >> 3)], m & 7, aH[2 * (2 + (m >> 3)) + ((m & 7) >> 2)],
                         aL[2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
+          sink_dword<kTrain>(sk, C0, 2 + (m >> 3), m >> 3, acc[2 + (m >> 3)], m & 7, h);
+        }
     }
     res = f32x4{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
-    res_p0 = p0;
+    if constexpr (kTrain) {
+      if (sk.valid && lane < 32) {
+        ((f32x4*)tro.rgbs)[p0] = f32x4{res[1], res[2], res[3], res[0]};
+        tro.hc[p0 * 132 + 128] = res[0];
+      }
+    } else {
+      res_p0 = p0;
+    }
   }
-  if (res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
+  if (!kTrain && res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
   wait_vmcnt(0);   // the stream ran into a tile that does not exist: let it land
 }
 
@@ -363,11 +411,21 @@ hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const Sample
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)
-    hipLaunchKernelGGL(mlp_bf16x3_kernel<true>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out);
+    hipLaunchKernelGGL((mlp_bf16x3_kernel<true, false>), grid, block, 0, stream, (const char*)blob, params, src,
+                       n_points, (f32x4*)out, X3TrainOut{});
   else
-    hipLaunchKernelGGL(mlp_bf16x3_kernel<false>, grid, block, 0, stream, (const char*)blob, params, src, n_points,
-                       (f32x4*)out);
+    hipLaunchKernelGGL((mlp_bf16x3_kernel<false, false>), grid, block, 0, stream, (const char*)blob, params, src,
+                       n_points, (f32x4*)out, X3TrainOut{});
+  return hipGetLastError();
+}
+
+hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
+                                   const X3TrainOut& o, hipStream_t stream) {
+  if (n_points <= 0) return hipSuccess;
+  const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
+  hipLaunchKernelGGL((mlp_bf16x3_kernel<false, true>), dim3(unsigned(blocks)), dim3(kThreads), 0, stream,
+                     (const char*)blob, params, src, n_points, (f32x4*)nullptr, o);
   return hipGetLastError();
 }
 

@@ -38,6 +38,18 @@ hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc
 // Split-bf16 parity-grade path (mlp_bf16x3.hip): (sigma, r, g, b) per sample.
 hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points,
                              float* out, bool explicit_points, hipStream_t stream);
+// The same kernel as the training forward (train.hip): per sample also every trunk layer's
+// post-ReLU row h[l] [P][256] and ReLU bit words mb[l] [P][8], the colour-0 row and density
+// hc [P][132], and (r, g, b, sigma) rgbs [P][4]; blob is the split-bf16 blob of the net's
+// current weights (nerf_pack_weights_bf16x3's layout), params the params blob.
+struct X3TrainOut {
+  float* h[8];
+  unsigned* mb[8];
+  float* hc;
+  float* rgbs;
+};
+hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
+                                   const X3TrainOut& o, hipStream_t stream);
 // Chains each ray's segment records into (rgb, depth) (nerf_device.h SegRecord).
 hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
                                      hipStream_t stream, OutStrides os = {});

@@ -1202,6 +1202,46 @@ inline unsigned blocks_for(long n, int per) { return unsigned((n + per - 1) / pe
 using namespace nerf;
 
 // ----------------------------------------------------------------- host --
+namespace nerf {
+namespace {
+// Flat parameters -> the split-bf16 blob of the forward (launch_mlp_bf16x3_train), both nets:
+// pack.cpp's nerf_pack_weights_bf16x3 element by element (stream element i of bf16 unit
+// n = i / 1024: layer l, quarter q, k-step u, tile-in-quarter o2, lane, j; then the heads'
+// units of two k-steps), W_hi = bf16(W) into unit 2n and W_lo = bf16(W - W_hi) into 2n + 1.
+constexpr int kX3UnitElems = kUnitBytes / 2;
+constexpr long kX3Elems = long(kHeadUnitBase + kHeadUnits) * kX3UnitElems;
+constexpr long kX3NetElems = kBf16x3BlobBytes / 2;
+__global__ void pack_x3_kernel(const float* __restrict__ params, unsigned short* __restrict__ blob) {
+  const long i = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= kX3Elems) return;
+  const float* prm = params + blockIdx.y * kNetFloats;
+  unsigned short* out = blob + blockIdx.y * kX3NetElems;
+  const int n = int(i / kX3UnitElems), off = int(i % kX3UnitElems);
+  const int lane = (off / 8) % 64, j = off % 8, half = off / 512;
+  float v = 0.0f;
+  if (n < kHeadUnitBase) {
+    int l = 0;
+    while (l + 1 < kNumMfmaLayers && bf16_unit_base(l + 1) <= n) ++l;
+    const int ku = ksteps_bf16(l), r = n - bf16_unit_base(l), q = r / ku, u = r % ku;
+    const int col = bf16_k_col(l, u, lane >> 5, j), row = 32 * (2 * q + half) + (lane & 31);
+    const int spec = l == C0 ? 9 : l;
+    const TensorDesc d = tensor_desc(2 * spec);
+    if (col >= 0) v = prm[d.off + long(row) * d.cols + col];
+  } else {
+    const int u = 2 * (n - kHeadUnitBase) + half, row = lane & 31;
+    int dens = 0;
+    const int f = head_k_row_col(u, row, lane >> 5, j, &dens);
+    if (f >= 0) v = dens ? prm[kFDensW + f] : prm[kFC1W + long(row) * kC0 + f];
+  }
+  const __bf16 hi = __bf16(v);                         // round to nearest even
+  const float hf = float(hi);
+  const __bf16 lo = __bf16(__fsub_rn(v, hf));          // exact in fp32
+  out[long(2 * n) * kX3UnitElems + off] = __builtin_bit_cast(unsigned short, hi);
+  out[long(2 * n + 1) * kX3UnitElems + off] = __builtin_bit_cast(unsigned short, lo);
+}
+}  // namespace
+}  // namespace nerf
+
 struct nerf_trainer {
   int device = 0;
   nerf_train_config cfg{};
@@ -1213,6 +1253,8 @@ struct nerf_trainer {
   float* m = nullptr;
   float* v = nullptr;
   float* gemmw = nullptr;    // [2][kGemmFloats]
+  unsigned short* x3 = nullptr;   // [2][kX3NetElems]: split-bf16 blob of the forward
+  bool fwd_x3 = false;            // forward on the split-bf16 MFMA (nerf_trainer_set_precision)
   float* ztab = nullptr;     // coarse table [n_coarse], fine table [n_fine]
   float* scal = nullptr;     // [0] clip coefficient, then double sum-of-squares partials
   int* bad = nullptr;        // device flag: a select index out of range
@@ -1236,6 +1278,16 @@ struct nerf_trainer {
 };
 
 namespace {
+
+// The kernels' operand copies of both nets' weights (after every change of the parameters).
+hipError_t pack_operands(nerf_trainer* tr, hipStream_t s) {
+  hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, s, (const float*)tr->params,
+                     tr->gemmw);
+  if (tr->fwd_x3)
+    hipLaunchKernelGGL(pack_x3_kernel, dim3(blocks_for(kX3Elems, 256), 2), dim3(256), 0, s, (const float*)tr->params,
+                       tr->x3);
+  return hipGetLastError();
+}
 
 constexpr int kSqBlocks = 256;
 
@@ -1432,9 +1484,17 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     fo.hc = a.hc;
     fo.rgbs = (f32x4*)a.rgbs;
     SampleSrc src{rays_o, rays_d, z, z_stride, S, nullptr, nullptr};
-    hipLaunchKernelGGL(train_fwd_kernel, dim3(blocks_for(P, 4 * kSamplesPerWave)), dim3(256), 0, s,
-                       (const f32x4*)(gw + kF32Blob), gw + kPrmBlob, src, P, fo);
-    HIP_TRY(hipGetLastError());
+    if (tr->fwd_x3) {
+      X3TrainOut xo;
+      for (int l = 0; l < 8; ++l) xo.h[l] = a.h[l], xo.mb[l] = a.mb[l];
+      xo.hc = a.hc;
+      xo.rgbs = a.rgbs;
+      HIP_TRY(launch_mlp_bf16x3_train(tr->x3 + net * kX3NetElems, gw + kPrmBlob, src, P, xo, s));
+    } else {
+      hipLaunchKernelGGL(train_fwd_kernel, dim3(blocks_for(P, 4 * kSamplesPerWave)), dim3(256), 0, s,
+                         (const f32x4*)(gw + kF32Blob), gw + kPrmBlob, src, P, fo);
+      HIP_TRY(hipGetLastError());
+    }
   }
   if ((rc = mark(2)) != NERF_OK) return rc;
   // volume render + loss, their backward (rendering.py:102-143, trainer.py:117-126)
@@ -1549,9 +1609,7 @@ int update_impl(nerf_trainer* tr, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, tr->params, tr->grads, tr->m, tr->v, n,
                      (const float*)tr->scal, aa);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, s, (const float*)tr->params,
-                     tr->gemmw);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(pack_operands(tr, s));
   tr->steps += 1;
   tr->lr = tr->lr * tr->cfg.lr_gamma;   // ExponentialLR.step: lr * gamma
   return NERF_OK;
@@ -1599,6 +1657,8 @@ int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* c
     if (hipMalloc((void**)p, bytes) != hipSuccess) return fail(set_error(NERF_E_HIP, "hipMalloc trainer state"));
   tr->grads = tr->own_grads;
   if (hipMalloc((void**)&tr->gemmw, sizeof(float) * 2 * kGemmFloats) != hipSuccess ||
+      hipMalloc((void**)&tr->x3, sizeof(unsigned short) * 2 * kX3NetElems) != hipSuccess ||
+      hipMemset(tr->x3, 0, sizeof(unsigned short) * 2 * kX3NetElems) != hipSuccess ||
       hipMalloc((void**)&tr->ztab, sizeof(float) * 2048) != hipSuccess ||
       hipMalloc((void**)&tr->scal, sizeof(float) * (4 + 2 * kSqBlocks)) != hipSuccess ||
       hipMalloc((void**)&tr->bad, sizeof(int)) != hipSuccess)
@@ -1632,9 +1692,7 @@ int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* c
       hipEventCreateWithFlags(&tr->join, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&tr->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_error(NERF_E_HIP, "trainer events / stream"));
-  hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, 0, (const float*)tr->params,
-                     tr->gemmw);
-  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+  if (pack_operands(tr, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fail(set_error(NERF_E_HIP, "trainer relayout failed"));
   *out = tr;
   return NERF_OK;
@@ -1647,6 +1705,7 @@ void nerf_trainer_destroy(nerf_trainer* tr) {
   for (float* p : {tr->params, tr->own_grads, tr->m, tr->v, tr->gemmw, tr->ztab, tr->scal, tr->ws, tr->part})
     if (p) (void)hipFree(p);
   if (tr->bad) (void)hipFree(tr->bad);
+  if (tr->x3) (void)hipFree(tr->x3);
   for (auto& e : tr->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {tr->done, tr->fork, tr->join})
@@ -1835,9 +1894,7 @@ int nerf_trainer_write(nerf_trainer* tr, int what, int net, const float* const* 
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(dst + net * kNetFloats, host.data(), sizeof(float) * kNetFloats, hipMemcpyHostToDevice));
   if (what == NERF_TR_PARAMS) {   // the kernels' operand copies of the weights
-    hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, 0,
-                       (const float*)tr->params, tr->gemmw);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(pack_operands(tr, 0));
     HIP_TRY(hipDeviceSynchronize());
   }
   return NERF_OK;
@@ -1848,6 +1905,18 @@ int nerf_trainer_set_schedule(nerf_trainer* tr, long steps, double lr) {
   if (steps < 0 || !(lr >= 0.0)) return set_error(NERF_E_INVALID, "nerf_trainer_set_schedule: steps %ld, lr %g", steps, lr);
   tr->steps = steps;
   tr->lr = lr;
+  return NERF_OK;
+}
+
+int nerf_trainer_set_precision(nerf_trainer* tr, int precision) {
+  if (!tr) return set_error(NERF_E_INVALID, "null trainer");
+  if (precision != NERF_FP32 && precision != NERF_BF16X3)
+    return set_error(NERF_E_INVALID, "nerf_trainer_set_precision: %d (NERF_FP32 or NERF_BF16X3)", precision);
+  DeviceGuardT dg(tr->device);
+  HIP_TRY(hipDeviceSynchronize());
+  tr->fwd_x3 = precision == NERF_BF16X3;
+  HIP_TRY(pack_operands(tr, 0));
+  HIP_TRY(hipDeviceSynchronize());
   return NERF_OK;
 }
 

@@ -84,6 +84,7 @@ SIGNATURES = {
     "nerf_trainer_write_grads": (_c.c_int, [_P, _c.c_int, _c.POINTER(_FP), _c.c_int]),
     "nerf_trainer_write": (_c.c_int, [_P, _c.c_int, _c.c_int, _c.POINTER(_FP), _c.c_int]),
     "nerf_trainer_set_schedule": (_c.c_int, [_P, _c.c_long, _c.c_double]),
+    "nerf_trainer_set_precision": (_c.c_int, [_P, _c.c_int]),
     "nerf_trainer_update": (_c.c_int, [_P, _P]),
     "nerf_trainer_lr": (_c.c_double, [_P]),
     "nerf_trainer_steps": (_c.c_long, [_P]),

@@ -112,6 +112,14 @@ class MI355XTrainer:
                                                ctypes.byref(h)))
         del kc, kf
         self._h = h
+        # the forward's arithmetic ("fp32": the reference's; "bf16x3": split bf16, faster,
+        # gradients as close to the float64 step as fp32's; include/nerf_mi355x.h)
+        self.precision = "fp32"
+        try:
+            self.set_precision(str(c.get("precision", "fp32")))
+        except ValueError:
+            self.close()
+            raise
         self._loss = torch.zeros(3, dtype=torch.float32, device=self.device)
         self._grad_t = None
         self._render_dev = None      # inference context for render_image / validate
@@ -260,6 +268,14 @@ class MI355XTrainer:
     @property
     def steps(self) -> int:
         return int(self.lib.nerf_trainer_steps(self._h))
+
+    def set_precision(self, precision: str) -> None:
+        """The forward's arithmetic: "fp32" (the reference's) or "bf16x3" (split bf16 on the
+        bf16 MFMA; nerf_trainer_set_precision in include/nerf_mi355x.h)."""
+        if precision not in ("fp32", "bf16x3"):
+            raise ValueError(f"precision {precision!r}: 'fp32' or 'bf16x3'")
+        rt._check(self.lib.nerf_trainer_set_precision(self._h, rt.PRECISIONS[precision]))
+        self.precision = precision
 
     def set_profiling(self, enable: bool) -> None:
         rt._check(self.lib.nerf_trainer_set_profiling(self._h, 1 if enable else 0))

@@ -175,3 +175,50 @@ class TrainOracle:
         for net, g in zip(self.nets, grads):
             for k in PARAM_ORDER:
                 net.p[k].grad = torch.as_tensor(np.asarray(g[k], dtype=np.float32)).clone()
+
+
+def step_grads_f64(sd_c, sd_f, image, pose, focal, sel, t_rand, config):
+    """One step's loss and both nets' gradients evaluated in float64: the ground truth that
+    an fp32 step (the reference's, this oracle's) and the GPU's split-bf16 step are each
+    measured against (tests/test_gpu_train.py, tools/train_diag.py).  The same graph as
+    TrainOracle.backward (nerf.py:24-45, 92-131; rendering.py:102-143; trainer.py:117-126)."""
+    dt = torch.float64
+    nets = [{k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in sd.items()}
+            for sd in (sd_c, sd_f)]
+
+    def lin(p, name, x):
+        return F.linear(x, p[f"{name}.weight"], p[f"{name}.bias"])
+
+    def pe(x, levels):
+        out = [x]
+        for k in range(levels):
+            a = (2.0 ** k) * np.pi * x
+            out += [torch.sin(a), torch.cos(a)]
+        return torch.cat(out, -1)
+
+    def fwd(p, pts, dirs):
+        e = pe(pts, 10)
+        x = e
+        for i in range(8):
+            if i == 4:
+                x = torch.cat([x, e], -1)
+            x = F.relu(lin(p, f"layers.{i}", x))
+        s = F.relu(lin(p, "density_head", x))
+        h = F.relu(lin(p, "color_layers.0", torch.cat([x, pe(dirs, 4)], -1)))
+        return s, torch.sigmoid(lin(p, "color_layers.1", h))
+
+    ro, rd = trainer_rays(pose, image.shape[0], image.shape[1], focal)
+    ro, rd = ro.reshape(-1, 3)[sel].to(dt), rd.reshape(-1, 3)[sel].to(dt)
+    tgt = torch.as_tensor(image).reshape(-1, 3)[sel].to(dt)
+    n = ro.shape[0]
+    zc = O.stratified_z(O.uniform_z(config["n_coarse"]), torch.as_tensor(t_rand).reshape(n, -1)).to(dt)
+    zf = O.uniform_z(config["n_fine"]).expand(n, config["n_fine"]).to(dt)
+    loss = 0
+    for p, z in zip(nets, (zc, zf)):
+        pts = ro[:, None, :] + rd[:, None, :] * z[..., None]
+        s, c = fwd(p, pts.reshape(-1, 3), rd[:, None, :].expand_as(pts).reshape(-1, 3))
+        rgb = volume_render_rgb(s.reshape(n, -1, 1), c.reshape(n, -1, 3), z, rd)
+        loss = loss + F.mse_loss(rgb, tgt)
+    loss.backward()
+    return float(loss), [{k: v.grad.numpy() for k, v in p.items()} for p in nets]
+

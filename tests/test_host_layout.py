@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.nerf_abi_version() == 3
+    assert lib.nerf_abi_version() == 4
 
 
 def test_uniform_z_bit_exact(golden):

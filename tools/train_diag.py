@@ -11,7 +11,6 @@ import sys
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "nerf-dbr_amd")]
@@ -22,48 +21,7 @@ from nerf_amd import weights as W  # noqa: E402
 from nerf_amd.trainer import MI355XTrainer  # noqa: E402
 
 
-def f64_grads(sd_c, sd_f, image, pose, focal, sel, t_rand, cfg):
-    """The same step in float64 (the ground truth for both fp32 runs)."""
-    dt = torch.float64
-    nets = []
-    for sd in (sd_c, sd_f):
-        nets.append({k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in sd.items()})
-
-    def lin(p, name, x):
-        return F.linear(x, p[f"{name}.weight"], p[f"{name}.bias"])
-
-    def pe(x, L):
-        out = [x]
-        for k in range(L):
-            a = (2.0 ** k) * np.pi * x
-            out += [torch.sin(a), torch.cos(a)]
-        return torch.cat(out, -1)
-
-    def fwd(p, pts, dirs):
-        e = pe(pts, 10)
-        x = e
-        for i in range(8):
-            if i == 4:
-                x = torch.cat([x, e], -1)
-            x = F.relu(lin(p, f"layers.{i}", x))
-        s = F.relu(lin(p, "density_head", x))
-        h = F.relu(lin(p, "color_layers.0", torch.cat([x, pe(dirs, 4)], -1)))
-        return s, torch.sigmoid(lin(p, "color_layers.1", h))
-
-    ro, rd = T.trainer_rays(pose, image.shape[0], image.shape[1], focal)
-    ro, rd = ro.reshape(-1, 3)[sel].to(dt), rd.reshape(-1, 3)[sel].to(dt)
-    tgt = torch.as_tensor(image).reshape(-1, 3)[sel].to(dt)
-    n = ro.shape[0]
-    zc = O.stratified_z(O.uniform_z(cfg["n_coarse"]), torch.as_tensor(t_rand).reshape(n, -1)).to(dt)
-    zf = O.uniform_z(cfg["n_fine"]).expand(n, cfg["n_fine"]).to(dt)
-    loss = 0
-    for p, z in zip(nets, (zc, zf)):
-        pts = ro[:, None, :] + rd[:, None, :] * z[..., None]
-        s, c = fwd(p, pts.reshape(-1, 3), rd[:, None, :].expand_as(pts).reshape(-1, 3))
-        rgb = T.volume_render_rgb(s.reshape(n, -1, 1), c.reshape(n, -1, 3), z, rd)
-        loss = loss + F.mse_loss(rgb, tgt)
-    loss.backward()
-    return float(loss), [{k: v.grad.numpy() for k, v in p.items()} for p in nets]
+f64_grads = T.step_grads_f64
 
 
 def rel(a, b):
