@@ -16,8 +16,8 @@ from nerf_amd import weights as W  # noqa: E402
 from nerf_amd.trainer import MI355XTrainer  # noqa: E402
 
 
-def main(steps=5):
-    cfg = {"lr": 3e-4, "weight_decay": 1e-6, "gradient_clipping": 1.0, "n_rays": 2048}
+def main(steps=5, precision="fp32"):
+    cfg = {"lr": 3e-4, "weight_decay": 1e-6, "gradient_clipping": 1.0, "n_rays": 2048, "precision": precision}
     sd_c, sd_f = W.synthetic_models(0)
     tr = MI355XTrainer(cfg, sd_c, sd_f)
     # profiling on: the two nets' passes run one after the other on one stream, so each
@@ -36,4 +36,4 @@ def main(steps=5):
 
 
 if __name__ == "__main__":
-    main(*[int(a) for a in sys.argv[1:]])
+    main(*[int(a) if a.isdigit() else a for a in sys.argv[1:]])   # [steps] [fp32|bf16x3]
