@@ -91,6 +91,126 @@ def frame_step(r, pose, width, height, spp, rank, world):
     return step, (r1 - r0) * width
 
 
+def check_gathered(r, pose, width, height, spp, rank, world):
+    """Outside any timed region: every rank renders its band into the packed tile, the tiles
+    are gathered to rank 0, and rank 0 renders the whole frame alone with the same renderer;
+    the two must agree bit for bit (a ray's result does not depend on which band it is in).
+    Returns the verdict on rank 0, None elsewhere."""
+    import torch
+
+    from nerf_amd import distributed as D
+
+    r0, r1 = D.band(rank, world, height)
+    tile = D.band_tile(world, height, width, r.torch_device())
+    r.render_band(pose, (width, height), spp, r0, r1, tile)
+    frame = D.gather_tiles_to_root(tile, width, height, copy=True)
+    if rank != 0:
+        return None
+    rgb = torch.empty(height, width, 3, device=r.torch_device())
+    dep = torch.empty(height, width, device=r.torch_device())
+    r.render_rows(pose, (width, height), spp, 0, height, rgb, dep)
+    torch.cuda.synchronize()
+    return {"gathered_equals_single": bool(torch.equal(frame[..., :3], rgb) and torch.equal(frame[..., 3], dep)),
+            "rgb_max_abs": float((frame[..., :3] - rgb).abs().max()),
+            "depth_max_abs": float((frame[..., 3] - dep).abs().max()),
+            "check": f"rank 0 rendered {width}x{height}x{spp} alone vs the {world} gathered band tiles"}
+
+
+def dist_record():
+    """The process group as it formed: backend, world size and the RCCL version."""
+    import torch
+    import torch.distributed as dist
+
+    rec = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+    if rec["backend"] == "nccl":
+        try:
+            rec["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception as e:            # noqa: BLE001 -- informational only
+            rec["rccl_version"] = f"unavailable: {e}"
+    return rec
+
+
+class ClockSampler:
+    """The GPU's graphics clock, power and hotspot temperature sampled with amdsmi every
+    ``period`` seconds in a thread while the timed frames run (so clock drift between runs
+    is attributable).  Fails soft: without amdsmi, or without access, ``summary()`` says why."""
+
+    KEYS = ("current_gfxclks", "current_gfxclk", "average_gfxclk_frequency", "current_socket_power",
+            "average_socket_power", "temperature_hotspot")
+
+    def __init__(self, device_index, period=0.02):
+        import threading
+
+        self.period, self.samples, self.error = period, [], None
+        self._stop = threading.Event()
+        self._thread = None
+        try:
+            import amdsmi
+            import torch
+
+            amdsmi.amdsmi_init()
+            self._smi = amdsmi
+            handles = amdsmi.amdsmi_get_processor_handles()
+            props = torch.cuda.get_device_properties(device_index)
+            want = (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", None))
+            self._h = None
+            for h in handles:
+                dom, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":", 1)
+                if (int(dom, 16), int(rest.split(":")[0], 16)) == want:
+                    self._h = h
+            if self._h is None and len(handles) == 1:
+                self._h = handles[0]
+            if self._h is None:
+                raise RuntimeError(f"no amdsmi handle matches PCI {want} among {len(handles)}")
+            self._thread = threading.Thread(target=self._run, daemon=True)
+        except Exception as e:            # noqa: BLE001 -- telemetry is optional
+            self.error = f"{type(e).__name__}: {e}"
+
+    def _read(self):
+        out = {}
+        try:
+            m = self._smi.amdsmi_get_gpu_metrics_info(self._h)
+            for k in self.KEYS:
+                v = m.get(k)
+                if isinstance(v, (list, tuple)):
+                    v = [x for x in v if isinstance(x, (int, float)) and 0 < x < 65535]
+                    v = sum(v) / len(v) if v else None
+                if isinstance(v, (int, float)) and 0 < v < 65535:
+                    out[k] = float(v)
+        except Exception as e:            # noqa: BLE001
+            self.error = f"{type(e).__name__}: {e}"
+        return out
+
+    def _run(self):
+        import time as _t
+
+        while not self._stop.is_set():
+            r = self._read()
+            if r:
+                self.samples.append(r)
+            _t.sleep(self.period)
+
+    def __enter__(self):
+        if self._thread is not None:
+            self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=5)
+
+    def summary(self):
+        out = {"source": "amdsmi_get_gpu_metrics_info", "samples": len(self.samples), "period_s": self.period}
+        if self.error:
+            out["error"] = self.error
+        for k in self.KEYS:
+            v = [smp[k] for smp in self.samples if k in smp]
+            if v:
+                out[k] = {"mean": sum(v) / len(v), "min": min(v), "max": max(v)}
+        return out
+
+
 def time_steps(step, n_warm, n_steps, world):
     """Max over ranks of the mean seconds per step (barrier + synchronize both sides)."""
     from nerf_amd import distributed as D
@@ -207,7 +327,8 @@ def sharded_hierarchical(ckpt, pose, local, rank, world, width, height, n_warm=2
     dt = time_steps(step, n_warm, n_steps, world)
     return {"rays_per_s": width * height / dt, "ms_per_frame": 1e3 * dt, "n_gpus": world,
             "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)",
-            "parallelism": f"row-band x{world} + {dist.get_backend()} gather to rank 0"}
+            "parallelism": f"row-band x{world} + {dist.get_backend()} gather to rank 0",
+            "self_check": check_gathered(h, pose, width, height, 64, rank, world)}
 
 
 # ---------------------------------------------------------------- training --
@@ -228,10 +349,9 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
 
     from nerf_amd import distributed as D
     from nerf_amd import weights as W
-    from nerf_amd.trainer import MI355XTrainer
-    from oracle import nerf_train_oracle as T
+    from nerf_amd.trainer import GEMM_MACS_PER_SAMPLE, MAIN_CONFIG, WGRAD_OPERAND_BYTES_PER_SAMPLE, MI355XTrainer
 
-    cfg = dict(T.TRAIN_CONFIG, n_rays=TRAIN_RAYS)
+    cfg = dict(MAIN_CONFIG, n_rays=TRAIN_RAYS)
     sd_c, sd_f = W.synthetic_models(0)
     tr = MI355XTrainer(cfg, sd_c, sd_f, device_index=local)
     h = w = 400
@@ -290,8 +410,23 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
           "note": "precision 'bf16x3': the forward on the split-bf16 MFMA (mlp_bf16x3.hip's kernel with the "
                   "rows and ReLU bits the backward reads); gradients as close to the float64 step as the "
                   "reference's fp32 step (tests/test_gpu_train.py); the default line above is fp32"}
-    gemm_ms = st["forward_gemm"] + st["backward_gemm"]
+    # per-kernel rates in the unit each kernel is bound by: the fused forward and the
+    # backward-data chain on the f32 MFMA, the weight gradients (split-bf16 MFMA) on HBM
+    samples = (int(TRAIN_RAYS) // world + (1 if rank < TRAIN_RAYS % world else 0)) * (cfg["n_coarse"] + cfg["n_fine"])
     flop = tr.gemm_flops()
+    assert abs(flop - 2.0 * sum(GEMM_MACS_PER_SAMPLE.values()) * samples) <= 1e-6 * flop, (flop, samples)
+    kernels = {}
+    for key, stage in (("forward", "forward_gemm"), ("backward_data", "backward_data_gemm")):
+        f = 2.0 * GEMM_MACS_PER_SAMPLE[key] * samples
+        kernels[key] = {"stage": stage, "ms": st[stage], "flop": f, "achieved": f / (st[stage] * 1e-3) / 1e12,
+                        "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                        "frac": f / (st[stage] * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"]}
+    b = WGRAD_OPERAND_BYTES_PER_SAMPLE * samples
+    kernels["weight_grad"] = {"stage": "weight_grad_gemm", "ms": st["weight_grad_gemm"], "bytes": b,
+                              "achieved": b / (st["weight_grad_gemm"] * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                              "frac": b / (st["weight_grad_gemm"] * 1e-3) / 1e9 / 8000.0,
+                              "note": "operand rows each weight-gradient GEMM reads (17,508 B per sample) over the "
+                                      "stage time; split-bf16 MFMA, bound by HBM"}
     out = {"workload": "NeRFTrainer.train_step, main.py config: 2048 rays of a 400x400 target, 64 stratified "
                        "coarse + 128 uniform fine samples, both nets forward+backward, clip 1.0, Adam, ExponentialLR",
            "dtype": "fp32 (weight-gradient GEMMs: split bf16, 3 bf16 MFMAs per fp32 product, fp32 accumulate)",
@@ -300,19 +435,16 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
            "parallelism": "1 GPU" if world == 1 else f"data parallel x{world}: 2048/{world} rays per rank + "
                                                      f"{'RCCL' if torch.distributed.get_backend() == 'nccl' else 'gloo'} "
                                                      f"all-reduce of the gradients (4.2 MB)",
-           "gemm": {"flop_per_step_rank0": flop, "ms_per_step": gemm_ms, "achieved": flop / (gemm_ms * 1e-3) / 1e12,
-                    "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
-                    "frac": flop / (gemm_ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"],
-                    "note": "all forward, backward-data and weight-gradient GEMMs of both nets (unpadded "
-                            "MACs x 2) over the forward_gemm + backward_gemm stages (HIP events of profiled "
-                            "steps, the two nets' passes one after the other), against the fp32 MFMA peak; "
-                            "the weight gradients run on the bf16 MFMA (split bf16) and are bound by HBM, "
-                            "so this is an fp32-equivalent rate (DESIGN.md section 10)"},
+           "gemm_kernels_rank0": kernels,
+           "gemm_note": "stage times from HIP events of profiled steps (the two nets' passes one after the "
+                        "other), both nets; unpadded GEMM work (trainer.GEMM_MACS_PER_SAMPLE) x samples",
            "loss_first_last": [losses[0], losses[-1]], "bf16x3_forward": x3}
     tr.close()
     if cpu_seconds > 0 and rank == 0 and world == 1:
         # the oracle's step (PyTorch-CPU autograd restatement of NeRFTrainer.train_step)
         import math
+
+        from oracle import nerf_train_oracle as T
 
         info = host_cpu_info()
         threads = info["physical_affinity"]
@@ -370,6 +502,12 @@ def host_cpu_info():
     return info
 
 
+def lego_psnr():
+    from nerf_amd import weights as W
+
+    return json.load(open(W.LEGO_NPZ.replace(".npz", ".json")))["report"]["fine"]["psnr_db_mean"]
+
+
 def cpu_baseline(budget_s):
     """The oracle's render_image on the host, the suite's protocol (wall clock around
     render_image including ray generation, averaged over the 2 views of
@@ -392,26 +530,37 @@ def cpu_baseline(budget_s):
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
-        _, fine = W.synthetic_models(0)
+        _, fine = W.lego_models()
         net = O.Net(fine)
         poses = generate_test_poses(2)
 
         def rate(width, height, spp, rows):
             r0 = (height - rows) // 2
-            t0 = time.perf_counter()
+            per_view = []
             for p in poses:
+                t0 = time.perf_counter()
                 O.render_image(net, p, (width, height), spp, rows=(r0, r0 + rows))
-            return rows * width * len(poses) / (time.perf_counter() - t0)
+                per_view.append(time.perf_counter() - t0)
+            return rows * width * len(poses) / sum(per_view), per_view
+
+        def loadavg():
+            try:
+                return [float(v) for v in open("/proc/loadavg").read().split()[:3]]
+            except OSError:
+                return None
 
         # calibrate each cell's rays/s on one row per view, then size its band
         cells = {}
         share = {"200x150x32": 0.2, "400x300x64": 0.3, "800x600x128": 0.5}
+        load0 = loadavg()
         for key, (w, h, s) in (("200x150x32", (200, 150, 32)), ("400x300x64", (400, 300, 64)),
                                ("800x600x128", (800, 600, 128))):
-            est = rate(w, h, s, 1)
+            est, _ = rate(w, h, s, 1)
             rows = int(min(h, max(2, share[key] * budget_s * est / (2 * w))))
-            v = rate(w, h, s, rows)
-            cells[key] = {"rays_per_s": v, "rows": rows, "rays_timed": 2 * rows * w}
+            v, per_view = rate(w, h, s, rows)
+            cells[key] = {"rays_per_s": v, "rows": rows, "rays_timed": 2 * rows * w,
+                          "seconds_per_view": per_view}
+        load1 = loadavg()
     finally:
         torch.set_num_threads(prev)
     head = cells["800x600x128"]
@@ -419,7 +568,8 @@ def cpu_baseline(budget_s):
             "sample": (f"oracle render_image (PyTorch-CPU restatement of PyTorchCPURenderer, 512-ray chunks), "
                        f"2 views of generate_test_poses(2), centre band of {head['rows']} rows of 800x600x128 "
                        f"per view ({head['rays_timed']} rays), {threads} torch threads, torch {torch.__version__}"),
-            "threads": threads, "host": info, "cells": cells}
+            "threads": threads, "host": info, "cells": cells,
+            "loadavg_1_5_15min": {"start": load0, "end": load1}}
 
 
 # --------------------------------------------------------------------- main --
@@ -441,10 +591,15 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank, world, local, dev = D.init_from_env()       # RCCL process group when world > 1
     local = dev
+    if world > 1:
+        # form the communicator before anything is timed (RCCL sets up lazily on first use)
+        warm = torch.ones(1, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(warm)
+        dist.barrier()
 
     width, height, spp = args.width, args.height, args.spp
     ckpt_dir = tempfile.mkdtemp(prefix=f"nerf_bench_r{rank}_")
-    ckpt = W.write_synthetic_checkpoint(os.path.join(ckpt_dir, "synthetic.pth"), seed=0)
+    ckpt = W.write_lego_checkpoint(os.path.join(ckpt_dir, "lego.pth"))
     r = MI355XRenderer(args.precision, device_index=local)
     r.setup(ckpt)
     r.hip.set_profiling(True)
@@ -456,11 +611,13 @@ def main():
     for _ in range(args.warmup):
         step()
     sync_barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()                                          # queued back to back: no host sync per frame
-    sync_barrier(world)
-    elapsed = D.reduce_max(time.perf_counter() - t0)   # max over ranks
+    clocks = ClockSampler(local)
+    with clocks:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()                                      # queued back to back: no host sync per frame
+        sync_barrier(world)
+        elapsed = D.reduce_max(time.perf_counter() - t0)   # max over ranks
     # the fine-MLP kernel's HIP-event times of the timed frames (the library's
     # per-frame event ring, recorded on the launch stream)
     kern_ms = kernel_ms(r, args.steps)
@@ -482,7 +639,10 @@ def main():
     achieved = flop_launch / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
 
-    extra = {}
+    extra = {"gpu_clock_timed_region": clocks.summary()}
+    if world > 1:
+        extra["dist"] = dist_record()
+        extra["self_check"] = check_gathered(r, pose, width, height, spp, rank, world)
     if world > 1 and not args.no_extras:
         # BASELINE config 4: the 64+128 hierarchical frame (bf16), sharded in row
         # bands over every rank and gathered to rank 0 -- every rank takes part
@@ -550,7 +710,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": args.precision,
-            "data": "synthetic: conditioned random-init NeRFModel weights (numpy seed 0), suite pose view 0",
+            "data": ("Lego: the reference's bundled original-NeRF Lego networks (data/lego_example_weights) "
+                     "distilled into NeRFModel's layout (nerf_amd/checkpoints/lego_distilled.npz, held-out PSNR "
+                     f"{lego_psnr():.1f} dB vs the teacher); suite pose view 0 (benchmark_suite.py:132-149); "
+                     "rays generated on the device from the pose"),
             "config": {"workload": f"render_image {width}x{height}, {spp} uniform samples/ray, fine net",
                        "resolution": [width, height], "samples_per_ray": spp,
                        "parallelism": (f"row-band x{world} + "

@@ -307,9 +307,10 @@ double nerf_trainer_lr(const nerf_trainer* tr);
 long nerf_trainer_steps(const nerf_trainer* tr);
 
 /* Per-stage device time of the last train_step (HIP events on the step's stream, profiling on):
- * 0 rays + sampling + encoding, 1 forward GEMMs, 2 colour head + volume render fwd/bwd,
- * 3 backward GEMMs, 4 gradient reduction + clip + Adam + weight relayout. */
-#define NERF_TRAIN_N_STAGES 5
+ * 0 rays + sampling + encoding, 1 forward GEMMs (f32 MFMA), 2 colour head + volume render
+ * fwd/bwd, 3 backward-data GEMMs (f32 MFMA) + the skinny head weight gradients, 4 weight-gradient
+ * GEMMs (split-bf16 MFMA, HBM-bound), 5 gradient reduction + clip + Adam + weight relayout. */
+#define NERF_TRAIN_N_STAGES 6
 int nerf_trainer_set_profiling(nerf_trainer* tr, int enable);
 int nerf_trainer_stage_ms(nerf_trainer* tr, float* ms_out /* [NERF_TRAIN_N_STAGES] */);
 /* Algorithmic fp32 FLOP of the last step's GEMMs (forward, backward-data, backward-weight,

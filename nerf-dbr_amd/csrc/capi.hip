@@ -483,6 +483,9 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
     ctx->last_zfine_rays = n_rays;
     ctx->last_zfine_per_ray = n_fine;
   } else {
+    // no importance stage: this render may overwrite where the last fine z lived
+    // (the stratified first-pass z shares the z buffer), so it is no longer readable
+    ctx->last_zfine = nullptr;
     if ((rc = mark(2)) != NERF_OK) return rc;
   }
   if ((rc = mark(3)) != NERF_OK) return rc;
@@ -538,8 +541,10 @@ int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, 
     return set_error(NERF_E_INVALID, "nerf_ctx_last_fine_z: the last hierarchical render had %ld rays x %d samples",
                      ctx->last_zfine_rays, ctx->last_zfine_per_ray);
   DeviceGuard g(ctx->device);
-  HIP_TRY(hipMemcpyAsync(z_out, ctx->last_zfine, sizeof(float) * size_t(n_rays) * per_ray, hipMemcpyDeviceToDevice,
-                         (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  if (s != ctx->last_stream)   // order the copy after the render that wrote the samples
+    HIP_TRY(hipStreamWaitEvent(s, ctx->frames[(ctx->n_frames - 1) % nerf_ctx::kEvFrames].ev[NERF_N_STAGES], 0));
+  HIP_TRY(hipMemcpyAsync(z_out, ctx->last_zfine, sizeof(float) * size_t(n_rays) * per_ray, hipMemcpyDeviceToDevice, s));
   return NERF_OK;
 }
 

@@ -1264,7 +1264,7 @@ struct nerf_trainer {
   size_t part_cap = 0;
   bool profiling = false;
   bool have_times = false;
-  hipEvent_t ev[12] = {};
+  hipEvent_t ev[14] = {};
   double gemm_flops = 0.0;
   // stream ordering: the workspace and state are reused by every call, so a call on a
   // stream other than the last one's waits for the last call's work (done)
@@ -1524,6 +1524,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
                        (const f32x4*)(gw + kBwdBlob), P, io);
     HIP_TRY(hipGetLastError());
   }
+  if ((rc = mark(4)) != NERF_OK) return rc;
   {
     // every weight-gradient GEMM of the net in one launch
     WGroup grp{};
@@ -1555,7 +1556,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
     hipLaunchKernelGGL(wgrad_group_kernel, dim3(nwg), dim3(512), 0, s, grp);
     HIP_TRY(hipGetLastError());
   }
-  if ((rc = mark(4)) != NERF_OK) return rc;
+  if ((rc = mark(5)) != NERF_OK) return rc;
 
   // partials -> flat gradients
   RedJobs jobs{};
@@ -1790,17 +1791,17 @@ int train_impl(nerf_trainer* tr, const float* image, int height, int width, floa
                      sc, 0, tr->ws + head, tr->part)) != NERF_OK)
     return rc;
   if (concurrent) HIP_TRY(hipEventRecord(tr->join, sc));
-  if ((rc = mark(5)) != NERF_OK) return rc;
+  if ((rc = mark(6)) != NERF_OK) return rc;
   if ((rc = net_pass(tr, 1, rays_o, rays_d, target, tr->ztab + 1024, 0, n_rays, n_total, tr->cfg.n_fine,
-                     loss_ray + n_rays, s, 5, tr->ws + head + acts_c, tr->part + parts_c)) != NERF_OK)
+                     loss_ray + n_rays, s, 6, tr->ws + head + acts_c, tr->part + parts_c)) != NERF_OK)
     return rc;
   if (concurrent) HIP_TRY(hipStreamWaitEvent(s, tr->join, 0));
-  if ((rc = mark(10)) != NERF_OK) return rc;
+  if ((rc = mark(12)) != NERF_OK) return rc;
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)loss_ray, n_rays, n_total,
                      (const double*)nullptr, 0, 0.0f, loss_out, (float*)nullptr);
   HIP_TRY(hipGetLastError());
   if (update && (rc = update_impl(tr, s)) != NERF_OK) return rc;
-  if ((rc = mark(11)) != NERF_OK) return rc;
+  if ((rc = mark(13)) != NERF_OK) return rc;
   tr->have_times = tr->profiling;
   return record_done(tr, s);
 }
@@ -1935,11 +1936,12 @@ int nerf_trainer_stage_ms(nerf_trainer* tr, float* ms_out) {
   for (int i = 0; i < NERF_TRAIN_N_STAGES; ++i) ms_out[i] = 0.0f;
   if (!tr->have_times) return NERF_OK;
   DeviceGuardT dg(tr->device);
-  HIP_TRY(hipEventSynchronize(tr->ev[11]));
-  // event order: 0 | encode c | 1 | fwd c | 2 | render c | 3 | bwd c | 4 | reduce c | 5 |
-  //              encode f | 6 | fwd f | 7 | render f | 8 | bwd f | 9 | reduce f | 10 | update | 11
-  static const int stage_of[11] = {0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 4};
-  for (int i = 0; i < 11; ++i) {
+  HIP_TRY(hipEventSynchronize(tr->ev[13]));
+  // event order: 0 | encode c | 1 | fwd c | 2 | render c | 3 | bwd-data c | 4 | wgrad c | 5 | reduce c | 6 |
+  //              encode f | 7 | fwd f | 8 | render f | 9 | bwd-data f | 10 | wgrad f | 11 | reduce f | 12 |
+  //              update | 13
+  static const int stage_of[13] = {0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 5};
+  for (int i = 0; i < 13; ++i) {
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, tr->ev[i], tr->ev[i + 1]));
     ms_out[stage_of[i]] += ms;

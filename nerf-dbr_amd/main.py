@@ -6,11 +6,12 @@ Same flags (``--data_dir --epochs --skip_training --checkpoint --benchmark_only`
 ``main.py:202-217``) and the same default grid (200x150 / 400x300 / 800x600 x 32 / 64 /
 128 spp, 2 views, ``main.py:134-141``).  Without ``--benchmark_only``/``--skip_training``
 it trains first, as ``train_nerf`` does (``main.py:65-109``), with ``MI355XTrainer`` and
-main.py's configuration; the dataset comes from the reference's own loader
-(``src.data.loader.load_synthetic_data``, importable when run from the reference checkout:
-the loader is not part of this package), and without it the CLI stops with a message.
-``--synthetic-checkpoint`` writes the deterministic conditioned checkpoint
-(nerf_amd.weights) first.
+main.py's configuration on the Blender-format dataset in ``--data_dir``
+(``nerf_amd.data.load_synthetic_data``, the contract of ``src/data/loader.py``).
+``--lego-checkpoint`` writes the distilled Lego checkpoint (``nerf_amd.weights``) to
+``--checkpoint`` first, ``--synthetic-checkpoint`` the deterministic conditioned one;
+both only with ``--benchmark_only`` / ``--skip_training`` (they would replace the
+trained model).
 """
 from __future__ import annotations
 
@@ -30,6 +31,8 @@ def main(argv=None) -> int:
     ap.add_argument("--benchmark_only", action="store_true")
     ap.add_argument("--synthetic-checkpoint", action="store_true",
                     help="write the deterministic synthetic checkpoint to --checkpoint first")
+    ap.add_argument("--lego-checkpoint", action="store_true",
+                    help="write the distilled Lego checkpoint to --checkpoint first")
     ap.add_argument("--resolutions", default="200x150,400x300,800x600")
     ap.add_argument("--spp", default="32,64,128")
     ap.add_argument("--views", type=int, default=2)
@@ -41,13 +44,14 @@ def main(argv=None) -> int:
     from nerf_amd import weights as W
     from nerf_amd.benchmark.benchmark_suite import UnifiedBenchmarkSuite
 
-    if not (args.skip_training or args.benchmark_only):
-        try:
-            from src.data.loader import load_synthetic_data   # the reference's loader (its checkout on the path)
-        except ImportError:
-            print("Training needs the reference's dataset loader (src/data/loader.py): run from the reference "
-                  "checkout, or use --benchmark_only with a reference-format checkpoint.")
-            return 1
+    train = not (args.skip_training or args.benchmark_only)
+    if train and (args.synthetic_checkpoint or args.lego_checkpoint):
+        ap.error("--synthetic-checkpoint / --lego-checkpoint replace the checkpoint: use them with "
+                 "--benchmark_only or --skip_training")
+    if args.synthetic_checkpoint and args.lego_checkpoint:
+        ap.error("--synthetic-checkpoint and --lego-checkpoint are exclusive")
+    if train:
+        from nerf_amd.data import load_synthetic_data
         from nerf_amd.trainer import MAIN_CONFIG, MI355XTrainer
 
         datasets = load_synthetic_data(args.data_dir, "cpu")
@@ -59,6 +63,8 @@ def main(argv=None) -> int:
         print(f"\nTraining completed! Model saved to: {args.checkpoint}")
     if args.synthetic_checkpoint:
         W.write_synthetic_checkpoint(args.checkpoint)
+    if args.lego_checkpoint:
+        W.write_lego_checkpoint(args.checkpoint)
     if not os.path.exists(args.checkpoint):
         print(f"Error: Checkpoint not found at {args.checkpoint}")
         return 1

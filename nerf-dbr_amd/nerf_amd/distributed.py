@@ -55,11 +55,16 @@ def band_tile(world: int, height: int, width: int, device):
     return _GATHER_BUFS[key]
 
 
-def gather_tiles_to_root(tile, width: int, height: int, root: int = 0, group=None):
+def gather_tiles_to_root(tile, width: int, height: int, root: int = 0, group=None, copy: bool = False):
     """Gather every rank's packed band tile ([max rows, W, 4]) to `root`: one
     ``dist.gather`` (RCCL: the root receives from each rank on its own xGMI link).
     Returns the frame as a packed [H, W, 4] tensor on the root (its views
-    [..., :3] and [..., 3] are the RGB and depth images), None elsewhere."""
+    [..., :3] and [..., 3] are the RGB and depth images), None elsewhere.
+
+    With ``copy=False`` (the frame loop's form: no allocation per frame) the result
+    ALIASES a receive buffer cached per shape whenever H divides evenly over the
+    ranks: it is valid until the next gather of the same shape, which overwrites it.
+    ``copy=True`` returns a tensor of its own in every case."""
     import torch
     import torch.distributed as dist
 
@@ -82,7 +87,8 @@ def gather_tiles_to_root(tile, width: int, height: int, root: int = 0, group=Non
     if rank != root:
         return None
     if height % world == 0:
-        return full.reshape(world * rows, width, 4)
+        frame = full.reshape(world * rows, width, 4)
+        return frame.clone() if copy else frame
     return torch.cat([full[r, : b1 - b0] for r, (b0, b1) in enumerate(bands(world, height))], 0)
 
 
@@ -160,7 +166,9 @@ def reduce_max(x: float) -> float:
 def render_frame_to_root(renderer, camera_pose, resolution: Tuple[int, int], samples_per_ray: int,
                          root: int = 0, group=None):
     """This rank renders its band into the packed tile (renderer.render_band) and the
-    tiles are gathered to `root`: (rgb [H,W,3], depth [H,W]) views on the root, None elsewhere."""
+    tiles are gathered to `root`: (rgb [H,W,3], depth [H,W]) on the root, None elsewhere.
+    The two are views of a frame tensor of their own (a later frame does not
+    overwrite them)."""
     import torch.distributed as dist
 
     width, height = resolution
@@ -169,7 +177,7 @@ def render_frame_to_root(renderer, camera_pose, resolution: Tuple[int, int], sam
     r0, r1 = band(rank, world, height)
     tile = band_tile(world, height, width, renderer.torch_device())
     renderer.render_band(camera_pose, resolution, samples_per_ray, r0, r1, tile)
-    full = gather_tiles_to_root(tile, width, height, root, group)
+    full = gather_tiles_to_root(tile, width, height, root, group, copy=True)
     return None if full is None else (full[..., :3], full[..., 3])
 
 

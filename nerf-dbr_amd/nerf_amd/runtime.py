@@ -104,8 +104,9 @@ class TrainConfig(_c.Structure):
 NERF_TRAIN_NO_UPDATE = 1
 NERF_TRAIN_NET_FLOATS = 530052
 NERF_TR_PARAMS, NERF_TR_GRADS, NERF_TR_EXP_AVG, NERF_TR_EXP_AVG_SQ = 0, 1, 2, 3
-NERF_TRAIN_N_STAGES = 5
-TRAIN_STAGES = ("rays_encode", "forward_gemm", "render_heads", "backward_gemm", "reduce_update")
+NERF_TRAIN_N_STAGES = 6
+TRAIN_STAGES = ("rays_encode", "forward_gemm", "render_heads", "backward_data_gemm", "weight_grad_gemm",
+                "reduce_update")
 
 _lib: Optional[ctypes.CDLL] = None
 

@@ -40,6 +40,15 @@ DEFAULTS = {
 }
 
 
+# Per-sample GEMM work of one net's training pass (train.hip gemm_macs_per_sample): the
+# forward and weight-gradient GEMMs cover the 8 trunk layers, colour-0 and density
+# (colour-1's 3 x 128 runs in the head kernels); backward-data skips the encodings' inputs.
+GEMM_MACS_PER_SAMPLE = {"forward": 527_488, "backward_data": 7 * 256 * 256 + 129 * 256, "weight_grad": 527_488}
+# Operand bytes the nine weight-gradient GEMMs read per sample, each GEMM's two row
+# operands once (dW = dZ^T [X | PE]): head 128 + 283, layer 0 256 + 63, layer 4 256 + 319,
+# six 256 x 256 layers; fp32.
+WGRAD_OPERAND_BYTES_PER_SAMPLE = 4 * ((128 + 283) + (256 + 63) + (256 + 319) + 6 * 512)
+
 # main.py:get_default_config (main.py:25-61), less the device key
 MAIN_CONFIG = {
     "lr": 3e-4,
@@ -414,10 +423,11 @@ class MI355XTrainer:
     def load_checkpoint(self, path: str) -> None:
         """NeRFTrainer.load_checkpoint (trainer.py:388-399): models, Adam's moments and step,
         the scheduler's learning rate and the loss histories, from a checkpoint written by the
-        reference trainer or by save_checkpoint (loaded with weights_only=True)."""
-        import torch
+        reference trainer or by save_checkpoint (loaded with weights_only=True, numpy scalars
+        admitted: the reference's loss histories are np.float64, trainer.py:336-345)."""
+        from .weights import torch_load_weights_only
 
-        ck = torch.load(path, map_location="cpu", weights_only=True)
+        ck = torch_load_weights_only(path)
         sds = [{k: v.detach().cpu().numpy().astype(np.float32) for k, v in ck[name].items()}
                for name in ("coarse_model", "fine_model")]
         for net, sd in enumerate(sds):
@@ -442,5 +452,5 @@ class MI355XTrainer:
         if sched is not None and "_last_lr" in sched:
             lr = float(sched["_last_lr"][0])
         self.set_schedule(steps, lr)
-        self.train_losses = list(ck.get("train_losses", []))
-        self.val_losses = list(ck.get("val_losses", []))
+        self.train_losses = [float(v) for v in ck.get("train_losses", [])]
+        self.val_losses = [float(v) for v in ck.get("val_losses", [])]

@@ -14,8 +14,10 @@ Checkpoints use the reference trainer's dict layout
 (``base_renderer.py:42``, ``weights_only=False``) checkpoints are loaded with
 ``torch.load(weights_only=True)``: nothing in a checkpoint file is executed.
 
-No trained checkpoint in this layout exists, and a randomly
-initialised net renders an all-black image.  ``synthetic_state_dict`` builds a
+The reference ships no trained checkpoint in this layout, and a randomly
+initialised net renders an all-black image.  Two checkpoints are provided: the
+Lego checkpoint (``lego_models``: the reference's bundled original-NeRF Lego
+networks distilled into this layout, see ``LEGO_NPZ``), and ``synthetic_state_dict``, a
 *conditioned* random net instead: ``nn.Linear``'s default
 init distribution (U(-1/sqrt(fan_in), 1/sqrt(fan_in)) for weight and bias) drawn
 from numpy's legacy ``RandomState`` (a stream numpy keeps stable across
@@ -129,17 +131,41 @@ def save_checkpoint(path: str, coarse: Mapping[str, np.ndarray], fine: Mapping[s
     return path
 
 
+def torch_load_weights_only(path: str):
+    """``torch.load(path, weights_only=True)`` that also admits numpy scalars.
+
+    The reference trainer stores its loss histories as ``np.float64`` values (they
+    come from ``np.mean``, ``src/training/trainer.py:336-345``), which the plain
+    weights-only unpickler refuses.  The scalar constructor and the float / int
+    dtype classes are added to its allowlist, under both the numpy-2 module path
+    and the ``numpy.core`` path older numpy writes; this admits data only, nothing
+    that executes."""
+    import torch
+
+    try:
+        import numpy._core.multiarray as ma
+    except ImportError:                                   # numpy < 2
+        import numpy.core.multiarray as ma
+    safe = [ma.scalar, (ma.scalar, "numpy.core.multiarray.scalar"), np.dtype]
+    for name in ("Float64DType", "Float32DType", "Int64DType", "Int32DType"):
+        cls = getattr(getattr(np, "dtypes", None), name, None)
+        if cls is not None:
+            safe.append(cls)
+    with torch.serialization.safe_globals(safe):
+        return torch.load(path, map_location="cpu", weights_only=True)
+
+
 def load_checkpoint(path: str) -> Tuple[StateDict, StateDict]:
     """Load ``(coarse, fine)`` from a reference-format checkpoint.
 
     Raises ``FileNotFoundError`` when the file is missing: unlike the reference
     (``base_renderer.py:62-76``) there is no silent random-weight fallback.
     """
-    import torch
-
     if not os.path.exists(path):
         raise FileNotFoundError(path)
-    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    if path.endswith(".npz"):              # the raw-array form (lego_distilled.npz)
+        return lego_models(path)
+    ckpt = torch_load_weights_only(path)
     coarse, fine = _to_numpy(ckpt["coarse_model"]), _to_numpy(ckpt["fine_model"])
     validate_state_dict(coarse)
     validate_state_dict(fine)
@@ -148,4 +174,29 @@ def load_checkpoint(path: str) -> Tuple[StateDict, StateDict]:
 
 def write_synthetic_checkpoint(path: str, seed: int = 0) -> str:
     coarse, fine = synthetic_models(seed)
+    return save_checkpoint(path, coarse, fine)
+
+
+# The Lego checkpoint: the reference's bundled original-NeRF Lego networks
+# (data/lego_example_weights/model{_fine,}_200000.npy) distilled into this layout by
+# tools/lego/distill.py (recipe, held-out PSNR vs the teacher: lego_distilled.json beside
+# it).  Raw fp32 arrays, no pickle: keys "coarse/<param>" and "fine/<param>".
+LEGO_NPZ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "checkpoints", "lego_distilled.npz")
+
+
+def lego_models(path: str = LEGO_NPZ) -> Tuple[StateDict, StateDict]:
+    """(coarse, fine) state dicts of the distilled Lego checkpoint."""
+    z = np.load(path, allow_pickle=False)
+    out = []
+    for net in ("coarse", "fine"):
+        sd = {k.split("/", 1)[1]: np.ascontiguousarray(z[k], dtype=np.float32) for k in z.files
+              if k.startswith(net + "/")}
+        validate_state_dict(sd)
+        out.append(sd)
+    return out[0], out[1]
+
+
+def write_lego_checkpoint(path: str) -> str:
+    """The distilled Lego checkpoint in the reference trainer's format (model entries)."""
+    coarse, fine = lego_models()
     return save_checkpoint(path, coarse, fine)

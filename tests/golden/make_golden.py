@@ -3,6 +3,7 @@
 Run in the development container only (the reference is not on the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --lego [/root/reference]
 
 It imports the reference's Python renderer, model and volume-render utilities
 (bypassing ``src/benchmark/__init__.py``, whose ``numba`` import is absent here
@@ -245,5 +246,84 @@ def main(ref_root: str = "/root/reference") -> None:
     print(json.dumps(meta, indent=1))
 
 
+def main_lego(ref_root: str = "/root/reference") -> None:
+    """Fixtures on the distilled Lego checkpoint (nerf_amd.weights.LEGO_NPZ, SURVEY §8f
+    row 1), rendered by the reference's own PyTorchCPURenderer: the BASELINE configs'
+    content.  lego_mlp.npz (NeRFModel.forward, both nets, points on rays through the
+    scene), render_lego_200x150_s32 (suite views 0, 1 + off-axis), render_lego_400x300_s64
+    (config 2: view 0 + off-axis) and a band of the 800x600x128 headline frame (rows
+    [296, 304), view 0 + off-axis)."""
+    import torch
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    PyTorchCPURenderer, NeRFModel, _, _ = import_reference(ref_root)
+    coarse_sd, fine_sd = W.lego_models()
+    ckpt_path = os.path.join(tempfile.mkdtemp(prefix="nerf_golden_lego_"), "lego.pth")
+    W.save_checkpoint(ckpt_path, coarse_sd, fine_sd)
+
+    def net(sd):
+        m = NeRFModel()
+        m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in sd.items()})
+        return m.eval()
+
+    coarse, fine = net(coarse_sd), net(fine_sd)
+    renderer = PyTorchCPURenderer()
+    renderer.setup(ckpt_path)
+    poses = suite_poses(2) + [off_axis_pose()]
+    pose_arr = np.stack([p.numpy() for p in poses])
+    save = lambda name, **kw: np.savez_compressed(os.path.join(HERE, name), **kw)  # noqa: E731
+    meta = {"torch": torch.__version__, "numpy": np.__version__, "checkpoint": "nerf_amd/checkpoints/lego_distilled.npz",
+            "coarse_digest": W.state_dict_digest(coarse_sd), "fine_digest": W.state_dict_digest(fine_sd),
+            "poses": "suite views 0,1 (benchmark_suite.py:132-149) + off-axis look-at"}
+
+    # MLP forward on points of rays through the scene (view 0 centre rows, off-axis centre rows)
+    pos, dirs = [], []
+    for pi in (0, 2):
+        ro, rd = renderer.generate_rays(poses[pi], 800, 600)
+        ro, rd = ro[300, 300:364].reshape(-1, 3), rd[300, 300:364].reshape(-1, 3)
+        pts, _ = renderer.sample_points_on_rays(ro, rd, 64)
+        pos.append(pts.reshape(-1, 3))
+        dirs.append(rd.repeat_interleave(64, 0))
+    pos, dirs = torch.cat(pos), torch.cat(dirs)
+    with torch.no_grad():
+        sf, cf = fine(pos, dirs)
+        sc, cc = coarse(pos, dirs)
+    save("lego_mlp.npz", pos=pos.numpy(), dirs=dirs.numpy(), sigma_fine=sf.numpy(), rgb_fine=cf.numpy(),
+         sigma_coarse=sc.numpy(), rgb_coarse=cc.numpy())
+
+    timing = {}
+    for (w, h, s, pose_ids) in [(200, 150, 32, [0, 1, 2]), (400, 300, 64, [0, 2])]:
+        out = {"poses": pose_arr[pose_ids], "pose_ids": np.array(pose_ids, dtype=np.int32),
+               "W": np.int32(w), "H": np.int32(h), "S": np.int32(s)}
+        for k, pi in enumerate(pose_ids):
+            t0 = time.time()
+            rgb, depth = renderer.render_image(poses[pi], (w, h), s)
+            timing[f"{w}x{h}x{s}_view{pi}"] = time.time() - t0
+            out[f"rgb_{k}"] = rgb.numpy()
+            out[f"depth_{k}"] = depth.numpy()
+        save(f"render_lego_{w}x{h}_s{s}.npz", **out)
+    band = {"rows": np.array([296, 304], dtype=np.int32), "W": np.int32(800), "H": np.int32(600),
+            "S": np.int32(128), "poses": pose_arr[[0, 2]]}
+    for k, pi in enumerate([0, 2]):
+        ro, rd = renderer.generate_rays(poses[pi], 800, 600)
+        ro, rd = ro[296:304].reshape(-1, 3), rd[296:304].reshape(-1, 3)
+        rgbs, depths = [], []
+        for c in range(0, ro.shape[0], 512):
+            r_, d_ = renderer._render_ray_chunk(ro[c:c + 512], rd[c:c + 512], 128)
+            rgbs.append(r_)
+            depths.append(d_)
+        band[f"rgb_{k}"] = torch.cat(rgbs).reshape(8, 800, 3).numpy()
+        band[f"depth_{k}"] = torch.cat(depths).reshape(8, 800).numpy()
+    save("render_lego_800x600_s128_band.npz", **band)
+    meta["render_seconds"] = timing
+    with open(os.path.join(HERE, "golden_lego_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1))
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--lego" in sys.argv:
+        main_lego(args[0] if args else "/root/reference")
+    else:
+        main(args[0] if args else "/root/reference")

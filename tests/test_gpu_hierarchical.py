@@ -135,3 +135,25 @@ def test_hierarchical_fused_coarse_handoff(ckpt, precision, res, nc):
     er, ed = maxabs(rgb_fused.reshape(-1, 3), rgb_ref), maxabs(dep_fused.reshape(-1), dep_ref)
     print(f"{precision} {res} {nc}+{ni}: render vs oracle composite of its fine samples: rgb {er:.2e} depth {ed:.2e}")
     assert er < 1e-5 and ed < 1e-4
+
+
+def test_last_fine_z_cleared_by_a_render_without_importance(ckpt):
+    """A render with n_importance = 0 may reuse the z buffer where the last fine z lived
+    (the stratified first-pass z shares it), so nerf_ctx_last_fine_z refuses afterwards
+    instead of returning overwritten depths; a copy on another stream is ordered after
+    the render that wrote the samples."""
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    r = MI355XRenderer("fp32", n_importance=32)
+    r.setup(ckpt)
+    pose = _pose(0)
+    r.render_image(pose, (16, 8), 32)
+    side = torch.cuda.Stream()
+    z = torch.empty(16 * 8, 64, dtype=torch.float32, device="cuda")
+    r.hip.last_fine_z(16 * 8, 64, z, stream=side)
+    side.synchronize()
+    assert bool((z[:, 1:] >= z[:, :-1]).all()) and float(z.min()) >= 2.0 and float(z.max()) <= 6.0
+    r.n_importance = 0
+    r.render_image(pose, (16, 8), 32)
+    with pytest.raises(RuntimeError):
+        r.hip.last_fine_z(16 * 8, 64, z)

@@ -173,10 +173,11 @@ def test_hierarchical_stage_by_stage(r32):
 
 
 def test_render_hierarchical_end_to_end(ckpt):
-    """Whole 64+128 render vs the oracle.  The fine samples are placed by the coarse
-    net's weights, so fp32 summation-order differences in the coarse MLP move them
-    (by ~1e-6 in z, amplified by the 2^9*pi position encoding); parity is therefore
-    asserted stage by stage above and only loosely here."""
+    """Whole 64+128 render at the parity gate: the fine samples are placed by the coarse
+    net's weights, so the chain is checked with the GPU's own coarse weights carried
+    forward (fp32 summation order moves a fine z by ~1e-6, amplified by the 2^9*pi
+    encoding): oracle sampler on them == the render's fine z (bit for bit), then the
+    oracle's fine pass on those samples within 1e-4 of the render."""
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
     from oracle import nerf_oracle as O
 
@@ -184,11 +185,22 @@ def test_render_hierarchical_end_to_end(ckpt):
     r.setup(ckpt)
     c, f = W.synthetic_models(0)
     pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][0])
-    rgb, depth = r.render_image(pose, (40, 30), 64)
-    ref_rgb, ref_depth = O.render_image_hierarchical(O.Net(c), O.Net(f), pose, (40, 30), 64, 128)
-    er, ed = maxabs(rgb, ref_rgb.numpy()), maxabs(depth, ref_depth.numpy())
+    w, h, nc, ni = 40, 30, 64, 128
+    rgb, depth = [t.clone() for t in r.render_image(pose, (w, h), nc)]
+    zf_render = torch.empty(w * h, nc + ni, dtype=torch.float32, device="cuda")
+    r.hip.last_fine_z(w * h, nc + ni, zf_render)
+    o, d = O.generate_rays(pose, w, h)
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    zc = O.uniform_z(nc).expand(w * h, nc).contiguous()
+    _, _, _, w_gpu = r.render_rays_z(o, d, zc, use_fine=False, with_weights=True)
+    zf = O.fine_z(zc, w_gpu.cpu(), O.default_u(w * h, ni))
+    assert torch.equal(zf, zf_render.cpu())
+    pts = O.sample_points(o, d, zf)
+    s_, c_ = O.nerf_forward(O.Net(f), pts.reshape(-1, 3), d[:, None].expand_as(pts).reshape(-1, 3))
+    ref_rgb, ref_depth = O.composite(s_.reshape(w * h, -1, 1), c_.reshape(w * h, -1, 3), zf, d)
+    er, ed = maxabs(rgb.reshape(-1, 3), ref_rgb.numpy()), maxabs(depth.reshape(-1), ref_depth.numpy())
     print(f"hierarchical end-to-end 40x30 64+128: rgb {er:.3e} depth {ed:.3e}")
-    assert er < 2e-2 and ed < 2e-2
+    assert er < TOL_RENDER and ed < TOL_RENDER
 
 
 def test_headline_full_size_properties(r16):
@@ -283,6 +295,8 @@ def test_render_stratified_hierarchical_stagewise(r32):
 
 
 def test_render_stratified_hierarchical_end_to_end(ckpt):
+    """Stratified coarse samples (injected t_rand) + per-ray importance draws (injected u):
+    the same chain as test_render_hierarchical_end_to_end at the 1e-4 gate."""
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
     from oracle import nerf_oracle as O
 
@@ -294,11 +308,21 @@ def test_render_stratified_hierarchical_end_to_end(ckpt):
     gen = torch.Generator().manual_seed(2)
     t_rand = torch.rand(w * h, nc, generator=gen)
     u = torch.sort(torch.rand(w * h, ni, generator=gen), -1).values
-    rgb, depth = r.render_rows(pose, (w, h), nc, 0, h, t_rand=t_rand, u=u)
-    ref_rgb, ref_depth = O.render_image_hierarchical(O.Net(c), O.Net(f), pose, (w, h), nc, ni, u=u, t_rand=t_rand)
-    er, ed = maxabs(rgb, ref_rgb.numpy()), maxabs(depth, ref_depth.numpy())
+    rgb, depth = [t.clone() for t in r.render_rows(pose, (w, h), nc, 0, h, t_rand=t_rand, u=u)]
+    zf_render = torch.empty(w * h, nc + ni, dtype=torch.float32, device="cuda")
+    r.hip.last_fine_z(w * h, nc + ni, zf_render)
+    o, d = O.generate_rays(pose, w, h)
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    zc = O.stratified_z(O.uniform_z(nc), t_rand).contiguous()
+    _, _, _, w_gpu = r.render_rays_z(o, d, zc, use_fine=False, with_weights=True)
+    zf = O.fine_z(zc, w_gpu.cpu(), u)
+    assert torch.equal(zf, zf_render.cpu())
+    pts = O.sample_points(o, d, zf)
+    s_, c_ = O.nerf_forward(O.Net(f), pts.reshape(-1, 3), d[:, None].expand_as(pts).reshape(-1, 3))
+    ref_rgb, ref_depth = O.composite(s_.reshape(w * h, -1, 1), c_.reshape(w * h, -1, 3), zf, d)
+    er, ed = maxabs(rgb.reshape(-1, 3), ref_rgb.numpy()), maxabs(depth.reshape(-1), ref_depth.numpy())
     print(f"stratified hierarchical end-to-end {w}x{h} {nc}+{ni}: rgb {er:.3e} depth {ed:.3e}")
-    assert er < 2e-2 and ed < 2e-2
+    assert er < TOL_RENDER and ed < TOL_RENDER
 
 
 # ------------------------------------------------------------ fp8 path (C5) --

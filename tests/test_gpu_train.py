@@ -395,58 +395,22 @@ def test_train_epoch_loop_checkpoints_and_resume(tmp_path):
     assert np.isfinite(v) and v > 0.0
 
 
-_FAKE_LOADER = '''
-import numpy as np
-import torch
-
-
-class _Set:
-    def __init__(self, n, seed):
-        rng = np.random.RandomState(seed)
-        self.items = []
-        for a in np.linspace(0.0, 1.0, n):
-            eye = np.array([3.0 * np.cos(a), 3.0 * np.sin(a), 1.5])
-            fwd = -eye / np.linalg.norm(eye)
-            right = np.cross(fwd, [0.0, 0.0, 1.0])
-            right /= np.linalg.norm(right)
-            c2w = np.eye(4)
-            c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = right, np.cross(right, fwd), -fwd, eye
-            self.items.append({"image": torch.from_numpy(rng.rand(10, 12, 3).astype(np.float32)),
-                               "pose": torch.from_numpy(c2w.astype(np.float32)), "focal": 11.0})
-
-    def __len__(self):
-        return len(self.items)
-
-    def __getitem__(self, i):
-        return self.items[i]
-
-
-def load_synthetic_data(data_dir, device="cpu"):
-    return {"train": _Set(2, 1), "val": _Set(1, 2)}
-'''
-
-
 def test_cli_trains_then_benchmarks(tmp_path, monkeypatch):
     """main.py without --benchmark_only: train_nerf (main.py:65-109) with MI355XTrainer and
-    main.py's configuration over the reference loader's datasets (a stand-in module here,
-    src.data.loader), then the benchmark on the checkpoint it wrote."""
+    main.py's configuration over a Blender-format dataset read by nerf_amd.data (the
+    loader.py contract), then the benchmark on the checkpoint it wrote."""
     import importlib
-    import sys
 
-    pkg = tmp_path / "ref"
-    (pkg / "src" / "data").mkdir(parents=True)
-    (pkg / "src" / "__init__.py").write_text("")
-    (pkg / "src" / "data" / "__init__.py").write_text("")
-    (pkg / "src" / "data" / "loader.py").write_text(_FAKE_LOADER)
-    monkeypatch.syspath_prepend(str(pkg))
-    for m in [m for m in sys.modules if m == "src" or m.startswith("src.")]:
-        monkeypatch.delitem(sys.modules, m)
+    from blender_fixture import write_blender_dataset
+
+    data = tmp_path / "lego_tiny"
+    write_blender_dataset(str(data), size=(12, 10))
     monkeypatch.chdir(tmp_path)
     import main as cli
     importlib.reload(cli)
     ck = tmp_path / "ck" / "final_model.pth"
-    rc = cli.main(["--epochs", "1", "--checkpoint", str(ck), "--resolutions", "24x16", "--spp", "8",
-                   "--views", "1", "--precisions", "fp32", "--output_dir", str(tmp_path / "out")])
+    rc = cli.main(["--data_dir", str(data), "--epochs", "1", "--checkpoint", str(ck), "--resolutions", "24x16",
+                   "--spp", "8", "--views", "1", "--precisions", "fp32", "--output_dir", str(tmp_path / "out")])
     assert rc in (0, None)
     ckd = torch.load(str(ck), weights_only=True)
     assert {"coarse_model", "fine_model", "optimizer", "scheduler"} <= set(ckd)

@@ -37,6 +37,64 @@ def test_checkpoint_reference_layout_with_extra_keys(tmp_path):
     assert W.state_dict_digest(f) == W.state_dict_digest(f2)
 
 
+@pytest.mark.parametrize("legacy_numpy_names", [False, True])
+def test_checkpoint_with_numpy_float64_losses(tmp_path, legacy_numpy_names):
+    """The reference trainer's loss histories are np.float64 (np.mean, trainer.py:336-345);
+    the weights-only loader admits them, also under the numpy<2 module path."""
+    import zipfile
+
+    c, f = W.synthetic_models(2)
+    ck = {"coarse_model": {k: torch.from_numpy(v) for k, v in c.items()},
+          "fine_model": {k: torch.from_numpy(v) for k, v in f.items()},
+          "train_losses": [np.mean([0.1, 0.2]), np.mean([0.05])], "val_losses": [np.float64(0.3)]}
+    p = str(tmp_path / "ref_trainer.pth")
+    torch.save(ck, p)
+    if legacy_numpy_names:
+        q = str(tmp_path / "ref_trainer_legacy.pth")
+        with zipfile.ZipFile(p) as zin, zipfile.ZipFile(q, "w", compression=zipfile.ZIP_STORED) as zout:
+            for it in zin.infolist():
+                data = zin.read(it.filename)
+                if it.filename.endswith("data.pkl"):
+                    assert b"numpy._core.multiarray" in data
+                    data = data.replace(b"numpy._core.multiarray", b"numpy.core.multiarray")
+                zout.writestr(it, data)
+        p = q
+    with pytest.raises(Exception):
+        torch.load(p, weights_only=True)            # what the plain weights-only load does
+    c2, f2 = W.load_checkpoint(p)
+    assert W.state_dict_digest(f) == W.state_dict_digest(f2)
+    raw = W.torch_load_weights_only(p)
+    assert [float(v) for v in raw["train_losses"]] == [0.15000000000000002, 0.05]
+
+
+def test_blender_loader_contract(tmp_path):
+    """nerf_amd.data follows src/data/loader.py:13-129: RGBA -> Lanczos resize -> /255 ->
+    white composite, focal from camera_angle_x, missing split skipped with a warning."""
+    from PIL import Image
+
+    from blender_fixture import write_blender_dataset
+    from nerf_amd.data import load_synthetic_data
+
+    raw = write_blender_dataset(str(tmp_path), splits=(("train", 2), ("test", 1)), size=(12, 10))
+    ds = load_synthetic_data(str(tmp_path), img_wh=(24, 20))
+    assert set(ds) == {"train", "test"}
+    tr = ds["train"]
+    assert len(tr) == 2 and np.isclose(tr.focal, 0.5 * 24 / np.tan(0.5 * 0.6911112070083618))
+    a = np.array(Image.fromarray(raw["train"][1], "RGBA").resize((24, 20), Image.LANCZOS)) / 255.0
+    want = a[..., :3] * a[..., 3:4] + (1 - a[..., 3:4])
+    item = tr[1]
+    assert item["image"].shape == (20, 24, 3) and item["pose"].shape == (4, 4)
+    assert np.allclose(item["image"].numpy(), want.astype(np.float32))
+
+
+def test_cli_refuses_to_overwrite_a_trained_model(tmp_path):
+    import main as cli
+
+    with pytest.raises(SystemExit):
+        cli.main(["--synthetic-checkpoint", "--checkpoint", str(tmp_path / "ck.pth")])
+    assert not os.path.exists(tmp_path / "ck.pth")
+
+
 def test_strict_state_dict():
     sd = W.synthetic_state_dict(0)
     del sd["density_head.bias"]
@@ -140,8 +198,21 @@ def _gather_worker(rank, world, port, width, height, q):
             out[: r1 - r0, :, 3] = d
             return out
 
-    root = D.render_frame_to_root(Tiler(), None, (width, height), 4)
-    root = None if root is None else (root[0].contiguous().numpy(), root[1].contiguous().numpy())
+    first = D.render_frame_to_root(Tiler(), None, (width, height), 4)
+    kept = None if first is None else (first[0].clone(), first[1].clone())
+
+    class Tiler2(Tiler):          # a second, different frame
+        def render_band(self, pose, res, spp, r0, r1, out):
+            super().render_band(pose, res, spp, r0, r1, out)
+            out[: r1 - r0] *= -1.0
+            return out
+
+    second = D.render_frame_to_root(Tiler2(), None, (width, height), 4)
+    if first is not None:
+        # the first frame the caller kept is not overwritten by the next gather
+        assert torch.equal(first[0], kept[0]) and torch.equal(first[1], kept[1])
+        assert torch.equal(second[0], -kept[0]) and torch.equal(second[1], -kept[1])
+    root = None if first is None else (first[0].contiguous().numpy(), first[1].contiguous().numpy())
     q.put((rank, rgb.numpy(), depth.numpy(), root))
     dist.barrier()
     dist.destroy_process_group()

@@ -141,3 +141,39 @@ def test_compressed_restatement_matches_reference(golden):
     assert np.array_equal(s.numpy(), g["sigma"]) and np.array_equal(c.numpy(), g["rgb"])
     rgb, depth = O.compressed_render_image(cw, torch.from_numpy(g["pose"]), (32, 24), 16)
     assert np.array_equal(rgb.numpy(), g["image"]) and np.array_equal(depth.numpy(), g["depth"])
+
+
+# ---- the Lego checkpoint: reference renders on real content ----------
+@pytest.fixture(scope="module")
+def lego_nets():
+    c, f = W.lego_models()
+    return O.Net(c), O.Net(f)
+
+
+def test_lego_checkpoint_digest_matches_fixtures():
+    meta = json.load(open(os.path.join(GOLDEN, "golden_lego_meta.json")))
+    c, f = W.lego_models()
+    assert W.state_dict_digest(c) == meta["coarse_digest"] and W.state_dict_digest(f) == meta["fine_digest"]
+
+
+def test_lego_mlp_forward(golden, lego_nets):
+    g = golden("lego_mlp")
+    coarse, fine = lego_nets
+    for net, tag in ((fine, "fine"), (coarse, "coarse")):
+        s, rgb = O.nerf_forward(net, torch.from_numpy(g["pos"]), torch.from_numpy(g["dirs"]))
+        np.testing.assert_allclose(s.numpy(), g[f"sigma_{tag}"], rtol=1e-5, atol=1e-4)
+        np.testing.assert_allclose(rgb.numpy(), g[f"rgb_{tag}"], rtol=0, atol=TOL)
+
+
+def test_lego_full_render_and_band(golden, lego_nets):
+    _, fine = lego_nets
+    g = golden("render_lego_200x150_s32")
+    for k in range(len(g["pose_ids"])):
+        rgb, depth = O.render_image(fine, g["poses"][k], (200, 150), 32)
+        np.testing.assert_allclose(rgb.numpy(), g[f"rgb_{k}"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(depth.numpy(), g[f"depth_{k}"], rtol=0, atol=1e-5)
+    g = golden("render_lego_800x600_s128_band")
+    r0, r1 = map(int, g["rows"])
+    rgb, depth = O.render_image(fine, g["poses"][1], (800, 600), 128, rows=(r0, r1))
+    np.testing.assert_allclose(rgb.numpy(), g["rgb_1"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(depth.numpy(), g["depth_1"], rtol=0, atol=1e-5)
