@@ -46,8 +46,11 @@ enum nerf_precision {
                     CompressedNeRFRenderer, src/benchmark/compressed_renderer.py) */
   NERF_BF16X3 = 3, /* split bf16 on the bf16 MFMA: W.X ~ Wh.Xh + Wh.Xl + Wl.Xh with
                       v = vh + vl, vh = bf16(v), vl = bf16(v - vh); f32 accumulate,
-                      accurate encodings: the parity-grade fast path (RGB/depth
+                      accurate encodings: a parity-grade fast path (RGB/depth
                       within the 1e-4 gate of the reference renderer) */
+  NERF_F16X3 = 4,  /* the same split on the f16 MFMA (v_mfma_f32_32x32x16_f16):
+                      11-bit halves, ~10x closer to fp32 than NERF_BF16X3 at the
+                      same MFMA count; weights must lie in fp16's range (65504) */
 };
 
 enum nerf_net { NERF_NET_COARSE = 0, NERF_NET_FINE = 1 };
@@ -91,6 +94,9 @@ void nerf_f32_to_e4m3(const float* x, int n, uint8_t* out);
  * NERF_BF16X3 kernel streams (nerf_layout.h kBf16x3BlobBytes). */
 size_t nerf_bf16x3_blob_bytes(void);
 int nerf_pack_weights_bf16x3(const float* const* params, int n_params, uint16_t* blob);
+/* The NERF_F16X3 blob (nerf_bf16x3_blob_bytes() bytes, the same unit layout with fp16
+ * halves: hi = f16(w), lo = f16(w - hi)); NERF_E_INVALID if a weight is outside fp16's range. */
+int nerf_pack_weights_f16x3(const float* const* params, int n_params, uint16_t* blob);
 
 /* Pure host helper: z = near*(1-t) + far*t in fp32, operation for operation
  * (src/benchmark/base_renderer.py:274-275). */

@@ -47,6 +47,8 @@ struct NetDev {
   void* bf16 = nullptr;
   void* fp8 = nullptr;      // e4m3 fragments + E8M0 row scales (nerf_layout.h)
   void* bf16x3 = nullptr;   // split-bf16 fragments: W_hi and W_lo units (nerf_layout.h)
+  void* f16x3 = nullptr;    // split-fp16 fragments, the same layout
+  bool f16x3_ok = false;    // the loaded weights fit fp16's range
   float* params = nullptr;
   bool loaded = false;
 };
@@ -109,9 +111,13 @@ int grow(T*& p, size_t& cap, size_t need, const char* what) {
 int check_net(nerf_ctx* ctx, int net, int precision) {
   if (!ctx) return set_error(NERF_E_INVALID, "null context");
   if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
-  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8 && precision != NERF_BF16X3)
+  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8 && precision != NERF_BF16X3 &&
+      precision != NERF_F16X3)
     return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (!ctx->net[net].loaded) return set_error(NERF_E_NO_WEIGHTS, "%s network not loaded", net ? "fine" : "coarse");
+  if (precision == NERF_F16X3 && !ctx->net[net].f16x3_ok)
+    return set_error(NERF_E_INVALID, "%s network has weights outside fp16's range: NERF_F16X3 unavailable",
+                     net ? "fine" : "coarse");
   return NERF_OK;
 }
 
@@ -131,7 +137,8 @@ hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, 
   const NetDev& nd = ctx->net[net];
   if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg, wloc);
-  if (precision == NERF_BF16X3) return launch_mlp_bf16x3(nd.bf16x3, nd.params, src, n, out, expl, s);
+  if (precision == NERF_BF16X3) return launch_mlp_bf16x3(nd.bf16x3, nd.params, src, n, out, expl, s, seg);
+  if (precision == NERF_F16X3) return launch_mlp_f16x3(nd.f16x3, nd.params, src, n, out, expl, s, seg);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
 }
 
@@ -181,6 +188,7 @@ void nerf_ctx_destroy(nerf_ctx* ctx) {
     if (nd.bf16) (void)hipFree(nd.bf16);
     if (nd.fp8) (void)hipFree(nd.fp8);
     if (nd.bf16x3) (void)hipFree(nd.bf16x3);
+    if (nd.f16x3) (void)hipFree(nd.f16x3);
     if (nd.params) (void)hipFree(nd.params);
   }
   for (float* p : {ctx->rays, ctx->mlp_out, ctx->zbuf, ctx->wbuf})
@@ -208,6 +216,9 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
   const size_t nx3 = nerf_bf16x3_blob_bytes();
   std::vector<uint16_t> x3(nx3 / 2);
   if ((rc = nerf_pack_weights_bf16x3(params, n_params, x3.data())) != NERF_OK) return rc;
+  // fp16 halves: only when every weight fits fp16's range (else NERF_F16X3 stays unavailable)
+  std::vector<uint16_t> h3(nx3 / 2);
+  const bool have_f16x3 = nerf_pack_weights_f16x3(params, n_params, h3.data()) == NERF_OK;
   DeviceGuard g(ctx->device);
   NetDev& nd = ctx->net[net];
   if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
@@ -217,6 +228,11 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
   if (!nd.bf16x3) HIP_TRY(hipMalloc(&nd.bf16x3, nx3));
   HIP_TRY(hipMemcpy(nd.fp8, f8.data(), nfp8, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.bf16x3, x3.data(), nx3, hipMemcpyHostToDevice));
+  if (have_f16x3) {
+    if (!nd.f16x3) HIP_TRY(hipMalloc(&nd.f16x3, nx3));
+    HIP_TRY(hipMemcpy(nd.f16x3, h3.data(), nx3, hipMemcpyHostToDevice));
+  }
+  nd.f16x3_ok = have_f16x3;
   HIP_TRY(hipMemcpy(nd.f32, f32.data(), nf32, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.bf16, bf.data(), nbf16, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));
@@ -489,11 +505,13 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
     if ((rc = mark(2)) != NERF_OK) return rc;
   }
   if ((rc = mark(3)) != NERF_OK) return rc;
-  // bf16 / fp8 with whole 32-sample segments per ray: compositing fused into the
-  // MLP epilogue (one record per segment), then chained per ray; the fp32 parity
-  // path keeps the sequential composite kernel
-  const bool fused = (ctx->fused_composite & 1) && (precision == NERF_BF16 || precision == NERF_FP8) && n_fine > 1 &&
-                     n_fine % 32 == 0;
+  // bf16 / fp8 / the split paths with whole 32-sample segments per ray: compositing
+  // fused into the MLP epilogue (one record per segment), then chained per ray; the
+  // fp32 parity path keeps the sequential composite kernel
+  const bool fused = (ctx->fused_composite & 1) &&
+                     (precision == NERF_BF16 || precision == NERF_FP8 || precision == NERF_BF16X3 ||
+                      precision == NERF_F16X3) &&
+                     n_fine > 1 && n_fine % 32 == 0;
   {
     SampleSrc src{rays_o, rays_d, z_main, z_stride, n_fine, nullptr, nullptr};
     HIP_TRY(run_mlp(ctx, net_main, precision, src, n_rays * n_fine, ctx->mlp_out, false, s,
@@ -549,7 +567,8 @@ int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, 
 }
 
 int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream) {
-  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8 && precision != NERF_BF16X3)
+  if (precision != NERF_FP32 && precision != NERF_BF16 && precision != NERF_FP8 && precision != NERF_BF16X3 &&
+      precision != NERF_F16X3)
     return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (n < 0 || (n_freqs != kPosL && n_freqs != kDirL))
     return set_error(NERF_E_INVALID, "nerf_positional_encoding: n %ld, n_freqs %d (the model's are 10 and 4)", n,

@@ -1,14 +1,19 @@
-// Split-bf16 ("bf16x3") NeRF MLP on gfx950: the parity-grade fast path.
+// Split-precision ("x3") NeRF MLP on gfx950: the parity-grade fast paths.
 //
 // Replaces NeRFModel.forward (src/models/nerf.py:92-131) fused with
 // sample_points_on_rays (src/benchmark/base_renderer.py:260-281) and the
-// positional encoding (nerf.py:24-45), like mlp_f32.hip, but on the bf16 MFMA
-// (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate): every fp32 operand v is
-// split into v_hi = bf16(v) and v_lo = bf16(v - v_hi), and each product is
+// positional encoding (nerf.py:24-45), like mlp_f32.hip, but on the 16-bit MFMA
+// (v_mfma_f32_32x32x16_{bf16,f16}, 16x the f32 MFMA rate): every fp32 operand v
+// is split into v_hi = T(v) and v_lo = T(v - v_hi), and each product is
 //     W.X ~= W_hi.X_hi + W_hi.X_lo + W_lo.X_hi
-// (the dropped W_lo.X_lo is ~2^-16 relative), accumulated in fp32.  Measured
-// against the reference PyTorch-CPU renderer this stays well inside the 1e-4
-// RGB/depth gate, at three bf16 MFMAs per product.
+// accumulated in fp32, three MFMAs per product.  Two operand types T:
+//   * bf16 (NERF_BF16X3): the dropped terms are ~2^-17 relative;
+//   * fp16 (NERF_F16X3): 11-bit halves, the dropped terms ~2^-22 relative (the
+//     lo parts of small values are fp16 subnormals: absolute 2^-25), ten times
+//     closer to fp32 than bf16x3 at the same MFMA count -- the margin the real
+//     (Lego) checkpoint needs under the 1e-4 gate.  fp16's range
+//     (65504) is checked on the weights at packing; activations of the NeRF MLP
+//     stay far inside it (max 65 on Lego, 6 on the synthetic net).
 //
 // Structure: mlp_bf16.hip's (transposed Linear, accumulators become the next
 // layer's B fragments, quarter schedule, LDS ring filled by LDS-DMA with one
@@ -18,13 +23,15 @@
 // fits in the 512-entry register file of a single wave (accumulators in AGPRs).
 //   * 4 waves x 32 samples = 128 samples per workgroup tile;
 //   * weight units of 4 KiB = the bf16 kernel's 2 KiB unit of W_hi, then W_lo
-//     (nerf_pack_weights_bf16x3), 4 units per 16 KiB chunk, 3-slot ring;
+//     (nerf_pack_weights_bf16x3 / _f16x3), 4 units per 16 KiB chunk, 3-slot ring;
 //   * encodings are the accurate fp32 ones (the fp32 path's sincosf), split
 //     into hi and lo fragments in LDS;
 //   * the ReLU'd fp32 activations are split as they are converted:
-//     hi = bf16(relu x), lo = bf16(relu x - hi).
-// Outputs (sigma, r, g, b) per sample; the render pass composites with the
-// sequential kernel (the fp32 path's).
+//     hi = T(relu x), lo = T(relu x - hi).
+// Outputs (sigma, r, g, b) per sample, or -- render passes with S % 32 == 0 --
+// the compositing fused into the epilogue: each wave's 32 samples are one
+// segment of one ray and leave as one 32-B segment record (nerf_device.h
+// seg_composite, chained by composite_segments_kernel), as mlp_bf16.hip does.
 #include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
@@ -63,7 +70,8 @@ constexpr int kLdsPeOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 10
 constexpr int kPeWaveB = 2 * 4 * 1024;                                // hi, lo x 4 k-steps x 1 KiB
 constexpr int kDeWaveB = 2 * 2 * 1024;                                // hi, lo x 2 k-steps x 1 KiB
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * kPeWaveB;
-constexpr int kLdsBytes = kLdsDeOff + kWaves * kDeWaveB;
+constexpr int kLdsSegOff = kLdsDeOff + kWaves * kDeWaveB;            // fused compositing: (dist, z) per sample
+constexpr int kLdsBytes = kLdsSegOff + kWaves * kSamplesPerWave * 8;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 // ds_read offsets are 16 bits: slots below kLoSlots are read at ring_addr + offset,
 // the rest at ring_hi_addr (= ring_addr + kLoSlots * kChunkB) + offset
@@ -73,7 +81,37 @@ static_assert(kGldsPerStage >= 1, "at least one LDS-DMA piece per wave per chunk
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// The operand type: the MFMA and the fp32 -> (hi, lo) split of two values, packed.
+struct OpBf16 {
+  typedef bf16x8 frag;
+  static __device__ __forceinline__ f32x16 mfma(const frag& a, const frag& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  // hi = bf16(v) (v_cvt_pk_bf16_f32), lo = bf16(v - hi); v - hi is exact in fp32
+  static __device__ __forceinline__ void split_pair(float a, float b, unsigned& hi, unsigned& lo) {
+    hi = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
+    const float ha = __builtin_bit_cast(float, hi << 16), hb = __builtin_bit_cast(float, hi & 0xFFFF0000u);
+    lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{__fsub_rn(a, ha), __fsub_rn(b, hb)}, bf16x2));
+  }
+};
+struct OpF16 {
+  typedef f16x8 frag;
+  static __device__ __forceinline__ f32x16 mfma(const frag& a, const frag& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  // hi = f16(v) (v_cvt_pk_f16_f32, round to nearest even), lo = f16(v - hi) (exact
+  // difference; subnormal lo for |v| < 2^-3 keeps an absolute 2^-25)
+  static __device__ __forceinline__ void split_pair(float a, float b, unsigned& hi, unsigned& lo) {
+    const f16x2 h = __builtin_convertvector(f32x2{a, b}, f16x2);
+    const f32x2 hf = __builtin_convertvector(h, f32x2);
+    hi = __builtin_bit_cast(unsigned, h);
+    lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{__fsub_rn(a, hf[0]), __fsub_rn(b, hf[1])}, f16x2));
+  }
+};
 
 // ---- compile-time unit map, as a constexpr table (this kernel is large
 // enough that the optimiser stops folding mlp_bf16.hip's loop-based map) ----
@@ -131,18 +169,12 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
                  lds_addr(dst + i * kThreads * 16));
 }
 
-// fp32 -> (hi, lo) bf16 parts of two values, packed: hi = bf16(v), lo = bf16(v - hi)
-__device__ __forceinline__ void split_pair(float a, float b, unsigned& hi, unsigned& lo) {
-  const bf16x2 p = __builtin_convertvector(f32x2{a, b}, bf16x2);                     // v_cvt_pk_bf16_f32
-  hi = __builtin_bit_cast(unsigned, p);
-  const float ha = __builtin_bit_cast(float, hi << 16), hb = __builtin_bit_cast(float, hi & 0xFFFF0000u);
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{__fsub_rn(a, ha), __fsub_rn(b, hb)}, bf16x2));
-}
+template <class Op>
 __device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     unsigned h2, l2;
-    split_pair(v[2 * d], v[2 * d + 1], h2, l2);
+    Op::split_pair(v[2 * d], v[2 * d + 1], h2, l2);
     hi[d] = h2;
     lo[d] = l2;
   }
@@ -150,21 +182,22 @@ __device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
 
 // Reads of unit n into ring entry n % kRing: A_hi and A_lo of the unit's two
 // output tiles and, for encoding inputs, the B fragment's hi and lo.
-__device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRing][4], bf16x8 (&rb)[kRing][2]) {
+template <class Op, class F = typename Op::frag>
+__device__ __forceinline__ void read_unit(const Ctx& cx, int n, F (&ra)[kRing][4], F (&rb)[kRing][2]) {
   const int slot = (n / kChunkUnits) % kSlots;
   const unsigned base = slot < kLoSlots ? cx.ring_addr : cx.ring_hi_addr;
   const int off = (slot < kLoSlots ? slot : slot - kLoSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
 #pragma unroll
-  for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<bf16x8>(base, off + f * 1024);
+  for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<F>(base, off + f * 1024);
   const int ex = kTab.u[n].extra;
   if (ex != 0) {
     const int u = kTab.u[n].kstep - layer_shape(kTab.u[n].layer).hidden / 16;
     if (ex == kPos) {
-      rb[n % kRing][0] = ds_read_b128<bf16x8>(cx.pe_addr, u * 1024);
-      rb[n % kRing][1] = ds_read_b128<bf16x8>(cx.pe_addr, 4096 + u * 1024);
+      rb[n % kRing][0] = ds_read_b128<F>(cx.pe_addr, u * 1024);
+      rb[n % kRing][1] = ds_read_b128<F>(cx.pe_addr, 4096 + u * 1024);
     } else {
-      rb[n % kRing][0] = ds_read_b128<bf16x8>(cx.de_addr, u * 1024);
-      rb[n % kRing][1] = ds_read_b128<bf16x8>(cx.de_addr, 2048 + u * 1024);
+      rb[n % kRing][0] = ds_read_b128<F>(cx.de_addr, u * 1024);
+      rb[n % kRing][1] = ds_read_b128<F>(cx.de_addr, 2048 + u * 1024);
     }
   }
 }
@@ -184,9 +217,10 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
 // Conversion schedule of mlp_bf16.hip: one dword (two values) per unit.
 NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
 NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
+template <class Op>
 __device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4& fhi, u32x4& flo) {
   unsigned h2, l2;
-  split_pair(relu(tile[2 * pr]), relu(tile[2 * pr + 1]), h2, l2);
+  Op::split_pair(relu(tile[2 * pr]), relu(tile[2 * pr + 1]), h2, l2);
   fhi[pr & 3] = h2;
   flo[pr & 3] = l2;
 }
@@ -202,11 +236,11 @@ __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (
   }
 }
 
-__device__ __forceinline__ f32x16 mfma3(const bf16x8& ahi, const bf16x8& alo, const bf16x8& bhi, const bf16x8& blo,
-                                        f32x16 acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc, 0, 0, 0);
+template <class Op, class F = typename Op::frag>
+__device__ __forceinline__ f32x16 mfma3(const F& ahi, const F& alo, const F& bhi, const F& blo, f32x16 acc) {
+  acc = Op::mfma(ahi, bhi, acc);
+  acc = Op::mfma(ahi, blo, acc);
+  return Op::mfma(alo, bhi, acc);
 }
 
 // Training outputs (launch_mlp_bf16x3_train): as each accumulator tile is converted, its
@@ -242,9 +276,9 @@ __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot
 }
 
 // One layer: reads the previous layer's fragments (ih/il), fills the next's (oh/ol).
-template <int L, bool kTrain>
+template <int L, bool kTrain, class Op, class F = typename Op::frag>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
-                                         u32x4 (&ol)[16], bf16x8 (&ra)[kRing][4], bf16x8 (&rb)[kRing][2],
+                                         u32x4 (&ol)[16], F (&ra)[kRing][4], F (&rb)[kRing][2],
                                          const Ctx& cx, TrainSink& sk) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
@@ -259,24 +293,24 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
       const int n = N0 + q * KU + u;
       seam_before(cx, n);
       if (u == 0) issue_bias(cx, L, q, acc);
-      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
       wait_lgkm(kTab.u[n].lgkm);
       __builtin_amdgcn_sched_barrier(0);
       const bool hid = u < KH;
-      const bf16x8 bhi = hid ? __builtin_bit_cast(bf16x8, ih[hid ? u : 0]) : rb[n % kRing][0];
-      const bf16x8 blo = hid ? __builtin_bit_cast(bf16x8, il[hid ? u : 0]) : rb[n % kRing][1];
+      const F bhi = hid ? __builtin_bit_cast(F, ih[hid ? u : 0]) : rb[n % kRing][0];
+      const F blo = hid ? __builtin_bit_cast(F, il[hid ? u : 0]) : rb[n % kRing][1];
 #pragma unroll
       for (int o2 = 0; o2 < 2; ++o2)
-        acc[2 * q + o2] = mfma3(ra[n % kRing][o2], ra[n % kRing][2 + o2], bhi, blo, acc[2 * q + o2]);
+        acc[2 * q + o2] = mfma3<Op>(ra[n % kRing][o2], ra[n % kRing][2 + o2], bhi, blo, acc[2 * q + o2]);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
         if (kConvert && q == 0 && u == dword_unit_in(m)) {
-          convert_dword(acc[6 + t], pr, ih[2 * (6 + t) + (pr >> 2)], il[2 * (6 + t) + (pr >> 2)]);
+          convert_dword<Op>(acc[6 + t], pr, ih[2 * (6 + t) + (pr >> 2)], il[2 * (6 + t) + (pr >> 2)]);
           sink_dword<kTrain>(sk, L > 0 ? L - 1 : 0, 6 + t, t, acc[6 + t], pr, cx.h);
         }
         if (q >= 1 && u == dword_unit_out(KU, m)) {
-          convert_dword(acc[2 * q - 2 + t], pr, oh[2 * (2 * q - 2 + t) + (pr >> 2)], ol[2 * (2 * q - 2 + t) + (pr >> 2)]);
+          convert_dword<Op>(acc[2 * q - 2 + t], pr, oh[2 * (2 * q - 2 + t) + (pr >> 2)], ol[2 * (2 * q - 2 + t) + (pr >> 2)]);
           sink_dword<kTrain>(sk, L, 2 * q - 2 + t, t, acc[2 * q - 2 + t], pr, cx.h);
         }
       }
@@ -284,11 +318,14 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
   }
 }
 
-template <bool kExplicit, bool kTrain>
-__global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __restrict__ blob,
-                                                                 const float* __restrict__ prm_g, SampleSrc src,
-                                                                 long n_points, f32x4* __restrict__ out,
-                                                                 X3TrainOut tro) {
+// seg != nullptr (render passes, S % 32 == 0): one segment record per wave's 32
+// samples instead of out's (sigma, r, g, b).
+template <bool kExplicit, bool kTrain, class Op>
+__global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restrict__ blob,
+                                                             const float* __restrict__ prm_g, SampleSrc src,
+                                                             long n_points, f32x4* __restrict__ out,
+                                                             f32x4* __restrict__ seg, X3TrainOut tro) {
+  typedef typename Op::frag F;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -298,6 +335,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
                 lds_base + kLdsDeOff + wave_u * kDeWaveB + lane * 16, lds_base + kLdsParamOff + h * 64,
                 lds_base + kLoSlots * kChunkB + lane * 16};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const bool fused = !kExplicit && !kTrain && seg != nullptr;
+  char* seg_slot = lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane & 31)) * 8;
 
 #pragma unroll
   for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
@@ -307,6 +346,17 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
 
   f32x4 res = {};
   long res_p0 = -1;
+  // the previous tile's results, stored after the next tile's first wait (vmcnt
+  // counts stores and LDS-DMA together, in issue order)
+  auto store = [&]() {
+    if (kTrain || res_p0 < 0) return;
+    if (fused) {
+      const long first = res_p0 - (lane & 31);                     // the segment's first sample
+      if (first < n_points && lane < 2) seg[(first / kSamplesPerWave) * 2 + lane] = res;
+    } else if (res_p0 < n_points && lane < 32) {
+      out[res_p0] = res;
+    }
+  };
 #pragma unroll 1
   for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const long p0 = (tile * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
@@ -315,7 +365,14 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
     TrainSink sk{tro, p0, p0 < n_points, {0u, 0u}};
     {
       float x[3], d[3], pef[32], def[16];
-      fetch_sample<kExplicit>(src, p0 < n_points ? p0 : n_points - 1, x, d);
+      const long pc = p0 < n_points ? p0 : n_points - 1;
+      if (fused) {
+        float dist, zz;
+        fetch_render_sample(src, pc, n_points <= 0xFFFFFFFFL, true, x, d, dist, zz);
+        if (h == 0) *(f32x2_t*)seg_slot = f32x2_t{dist, zz};
+      } else {
+        fetch_sample<kExplicit>(src, pc, x, d);
+      }
       pos_encode<false>(x[0], x[1], x[2], h, pef);    // accurate sincosf, as the fp32 path
       dir_encode<false>(d[0], d[1], d[2], h, def);
       char* pe_dst = lds + kLdsPeOff + wave_u * kPeWaveB + lane * 16;
@@ -323,14 +380,14 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         u32x4 hi, lo;
-        split8(pef + 8 * u, hi, lo);
+        split8<Op>(pef + 8 * u, hi, lo);
         *(u32x4*)(pe_dst + u * 1024) = hi;
         *(u32x4*)(pe_dst + 4096 + u * 1024) = lo;
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         u32x4 hi, lo;
-        split8(def + 8 * u, hi, lo);
+        split8<Op>(def + 8 * u, hi, lo);
         *(u32x4*)(de_dst + u * 1024) = hi;
         *(u32x4*)(de_dst + 2048 + u * 1024) = lo;
       }
@@ -338,22 +395,22 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
     wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
     stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
-    if (!kTrain && res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
-    bf16x8 ra[kRing][4], rb[kRing][2];
+    store();
+    F ra[kRing][4], rb[kRing][2];
     f32x16 acc[8];
 #pragma unroll
-    for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+    for (int n = 0; n < kPf; ++n) read_unit<Op>(cx, n, ra, rb);
 
     u32x4 aH[16], aL[16], bH[16], bL[16];
-    layer_x3<L0, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
-    layer_x3<L1, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<L2, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
-    layer_x3<L3, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<L4, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // skip: [x, pe] (nerf.py:109-110)
-    layer_x3<L5, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<L6, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
-    layer_x3<L7, kTrain>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<C0, kTrain>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // [x, PE4(d)] (nerf.py:117-121)
+    layer_x3<L0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
+    layer_x3<L1, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<L2, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
+    layer_x3<L3, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<L4, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // skip: [x, pe] (nerf.py:109-110)
+    layer_x3<L5, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<L6, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
+    layer_x3<L7, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
+    layer_x3<C0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // [x, PE4(d)] (nerf.py:117-121)
 
     // Heads (nerf.py:114, 123-129): one tile, density row 3 over L7's fragments
     // (bH/bL, C0's input, k-steps 0..15), colour rows 0-2 over C0's output
@@ -369,22 +426,22 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
     for (int i = 0; i < kHeadUnits; ++i) {
       const int n = kHeadUnitBase + i;
       seam_before(cx, n);
-      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
       wait_lgkm(4 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int k = 2 * i + s2;
-        const bf16x8 bhi = __builtin_bit_cast(bf16x8, k < 16 ? bH[k < 16 ? k : 0] : aH[k >= 16 ? k - 16 : 0]);
-        const bf16x8 blo = __builtin_bit_cast(bf16x8, k < 16 ? bL[k < 16 ? k : 0] : aL[k >= 16 ? k - 16 : 0]);
-        hacc = mfma3(ra[n % kRing][s2], ra[n % kRing][2 + s2], bhi, blo, hacc);
+        const F bhi = __builtin_bit_cast(F, k < 16 ? bH[k < 16 ? k : 0] : aH[k >= 16 ? k - 16 : 0]);
+        const F blo = __builtin_bit_cast(F, k < 16 ? bL[k < 16 ? k : 0] : aL[k >= 16 ? k - 16 : 0]);
+        hacc = mfma3<Op>(ra[n % kRing][s2], ra[n % kRing][2 + s2], bhi, blo, hacc);
       }
 #pragma unroll
       for (int m = 0; m < 16; ++m)
         if (i < 8 && m / 2 == i)
           {
-          convert_dword(acc[2 + (m >> 3)], m & 7, aH[2 * (2 + (m >> 3)) + ((m & 7) >> 2)],
-                        aL[2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
+          convert_dword<Op>(acc[2 + (m >> 3)], m & 7, aH[2 * (2 + (m >> 3)) + ((m & 7) >> 2)],
+                            aL[2 * (2 + (m >> 3)) + ((m & 7) >> 2)]);
           sink_dword<kTrain>(sk, C0, 2 + (m >> 3), m >> 3, acc[2 + (m >> 3)], m & 7, h);
         }
     }
@@ -395,28 +452,45 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16x3_kernel(const char* __r
         tro.hc[p0 * 132 + 128] = res[0];
       }
     } else {
+      if (fused) {
+        const f32x2_t in = *(const f32x2_t*)seg_slot;
+        float wl;
+        res = seg_composite(res, in[0], in[1], lane, wl);
+      }
       res_p0 = p0;
     }
   }
-  if (!kTrain && res_p0 >= 0 && res_p0 < n_points && lane < 32) out[res_p0] = res;
+  store();
   wait_vmcnt(0);   // the stream ran into a tile that does not exist: let it land
+}
+
+template <class Op>
+hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
+                     bool explicit_points, hipStream_t stream, float* seg) {
+  if (n_points <= 0) return hipSuccess;
+  if (seg != nullptr && (explicit_points || src.n_samples % kSamplesPerWave != 0)) return hipErrorInvalidValue;
+  const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
+  const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
+  if (explicit_points)
+    hipLaunchKernelGGL((mlp_x3_kernel<true, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,
+                       n_points, (f32x4*)out, (f32x4*)nullptr, X3TrainOut{});
+  else
+    hipLaunchKernelGGL((mlp_x3_kernel<false, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,
+                       n_points, (f32x4*)out, (f32x4*)seg, X3TrainOut{});
+  return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                             bool explicit_points, hipStream_t stream) {
-  if (n_points <= 0) return hipSuccess;
-  const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
-  const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
-  const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
-  if (explicit_points)
-    hipLaunchKernelGGL((mlp_bf16x3_kernel<true, false>), grid, block, 0, stream, (const char*)blob, params, src,
-                       n_points, (f32x4*)out, X3TrainOut{});
-  else
-    hipLaunchKernelGGL((mlp_bf16x3_kernel<false, false>), grid, block, 0, stream, (const char*)blob, params, src,
-                       n_points, (f32x4*)out, X3TrainOut{});
-  return hipGetLastError();
+                             bool explicit_points, hipStream_t stream, float* seg) {
+  return launch_x3<OpBf16>(blob, params, src, n_points, out, explicit_points, stream, seg);
+}
+
+hipError_t launch_mlp_f16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
+                            bool explicit_points, hipStream_t stream, float* seg) {
+  return launch_x3<OpF16>(blob, params, src, n_points, out, explicit_points, stream, seg);
 }
 
 hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
@@ -424,8 +498,8 @@ hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const 
   if (n_points <= 0) return hipSuccess;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
-  hipLaunchKernelGGL((mlp_bf16x3_kernel<false, true>), dim3(unsigned(blocks)), dim3(kThreads), 0, stream,
-                     (const char*)blob, params, src, n_points, (f32x4*)nullptr, o);
+  hipLaunchKernelGGL((mlp_x3_kernel<false, true, OpBf16>), dim3(unsigned(blocks)), dim3(kThreads), 0, stream,
+                     (const char*)blob, params, src, n_points, (f32x4*)nullptr, (f32x4*)nullptr, o);
   return hipGetLastError();
 }
 

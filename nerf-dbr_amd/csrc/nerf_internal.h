@@ -37,7 +37,11 @@ hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc
                           float* wloc = nullptr);
 // Split-bf16 parity-grade path (mlp_bf16x3.hip): (sigma, r, g, b) per sample.
 hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points,
-                             float* out, bool explicit_points, hipStream_t stream);
+                             float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr);
+// Split-fp16 parity-grade path (the same kernel on the f16 MFMA, nerf_pack_weights_f16x3's blob).
+// seg: the render pass's fused compositing (S % 32 == 0), one SegRecord per 32 samples.
+hipError_t launch_mlp_f16x3(const void* blob, const float* params, const SampleSrc& src, long n_points,
+                            float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr);
 // The same kernel as the training forward (train.hip): per sample also every trunk layer's
 // post-ReLU row h[l] [P][256] and ReLU bit words mb[l] [P][8], the colour-0 row and density
 // hc [P][132], and (r, g, b, sigma) rgbs [P][4]; blob is the split-bf16 blob of the net's

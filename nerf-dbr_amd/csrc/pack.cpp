@@ -115,6 +115,27 @@ extern "C" int nerf_pack_weights_bf16x3(const float* const* params, int n_params
   return NERF_OK;
 }
 
+extern "C" int nerf_pack_weights_f16x3(const float* const* params, int n_params, uint16_t* blob) {
+  if (!params || n_params != NERF_N_PARAMS || !blob)
+    return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: need %d tensors and a blob", NERF_N_PARAMS);
+  for (int i = 0; i < NERF_N_PARAMS; ++i)
+    if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: tensor %d is NULL", i);
+  std::vector<float> vals;
+  bf16_stream_values(params, vals);
+  constexpr size_t kUnit = size_t(kUnitBytes) / 2;          // 16-bit elements per unit
+  std::memset(blob, 0, size_t(kBf16x3BlobBytes));
+  for (size_t i = 0; i < vals.size(); ++i) {
+    if (!(std::fabs(vals[i]) <= 65504.0f))
+      return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: weight %g is outside the fp16 range", double(vals[i]));
+    const _Float16 hi = _Float16(vals[i]);                  // round to nearest even
+    const _Float16 lo = _Float16(vals[i] - float(hi));      // the difference is exact in fp32
+    const size_t unit = i / kUnit, off = i % kUnit;
+    std::memcpy(&blob[(2 * unit) * kUnit + off], &hi, 2);
+    std::memcpy(&blob[(2 * unit + 1) * kUnit + off], &lo, 2);
+  }
+  return NERF_OK;
+}
+
 extern "C" size_t nerf_fp8_blob_bytes(void) { return size_t(kFp8BlobBytes); }
 
 extern "C" void nerf_f32_to_e4m3(const float* x, int n, uint8_t* out) {

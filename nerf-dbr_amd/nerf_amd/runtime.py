@@ -24,14 +24,14 @@ LIB_NAME = "libnerf_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", LIB_NAME)
 
 NERF_OK = 0
-NERF_FP32, NERF_BF16, NERF_FP8, NERF_BF16X3 = 0, 1, 2, 3
+NERF_FP32, NERF_BF16, NERF_FP8, NERF_BF16X3, NERF_F16X3 = 0, 1, 2, 3, 4
 NERF_NET_COARSE, NERF_NET_FINE = 0, 1
 NERF_N_PARAMS = 22
 NERF_N_STAGES = 5
 NERF_OPT_FUSED_COMPOSITE = 1
 STAGES = ("rays", "coarse_mlp", "importance", "fine_mlp", "composite")
 
-PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16, "fp8": NERF_FP8, "bf16x3": NERF_BF16X3}
+PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16, "fp8": NERF_FP8, "bf16x3": NERF_BF16X3, "f16x3": NERF_F16X3}
 
 # Every symbol include/nerf_mi355x.h declares, with its ctypes signature.
 _c = ctypes
@@ -72,6 +72,7 @@ SIGNATURES = {
     "nerf_positional_encoding": (_c.c_int, [_c.c_int, _P, _c.c_long, _c.c_int, _P, _P]),
     "nerf_bf16x3_blob_bytes": (_c.c_size_t, []),
     "nerf_pack_weights_bf16x3": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P]),
+    "nerf_pack_weights_f16x3": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P]),
     "nerf_linspace01": (None, [_c.c_int, _FP]),
     "nerf_trainer_create": (_c.c_int, [_c.c_int, _P, _c.POINTER(_FP), _c.POINTER(_FP), _c.c_int, _c.POINTER(_P)]),
     "nerf_trainer_destroy": (None, [_P]),
@@ -178,6 +179,16 @@ def pack_weights_fp8(sd: Mapping[str, np.ndarray]) -> np.ndarray:
     blob = np.zeros(lib.nerf_fp8_blob_bytes(), np.uint8)
     keep, ptrs = _param_list(sd)
     _check(lib.nerf_pack_weights_fp8(ptrs, NERF_N_PARAMS, blob.ctypes.data_as(_P)))
+    del keep
+    return blob
+
+
+def pack_weights_f16x3(sd: Mapping[str, np.ndarray]) -> np.ndarray:
+    """Host-only split-fp16 packing (fp16 W_hi and W_lo units, uint16), as the loader runs it."""
+    lib = load_library()
+    blob = np.zeros(lib.nerf_bf16x3_blob_bytes() // 2, np.uint16)
+    keep, ptrs = _param_list(sd)
+    _check(lib.nerf_pack_weights_f16x3(ptrs, NERF_N_PARAMS, blob.ctypes.data_as(_P)))
     del keep
     return blob
 

@@ -471,7 +471,10 @@ def test_bench_single_gpu_json_contract():
     assert cb["kind"] == "port" and cb["unit"] == "rays/s" and cb["value"] > 0 and cb["cores"] >= 1
     t = b["training"]                                 # the training-step leg
     assert t["n_gpus"] == 1 and t["rays_per_s"] == pytest.approx(2048 / (t["ms_per_step"] * 1e-3), rel=1e-6)
-    assert 0 < t["gemm"]["frac"] < 1 and t["gemm"]["peak"] == 157.3
+    gk = t["gemm_kernels_rank0"]
+    for key in ("forward", "backward_data"):
+        assert 0 < gk[key]["frac"] < 1 and gk[key]["peak"] == 157.3 and gk[key]["unit"] == "TFLOP/s"
+    assert 0 < gk["weight_grad"]["frac"] < 1 and gk["weight_grad"]["peak"] == 8000.0 and gk["weight_grad"]["unit"] == "GB/s"
     assert t["cpu_baseline"]["kind"] == "port" and t["cpu_baseline"]["value"] > 0
     assert t["loss_first_last"][-1] < t["loss_first_last"][0]
 
