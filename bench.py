@@ -31,10 +31,10 @@ for _p in (REPO, os.path.join(REPO, "nerf-dbr_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-# MI355X dense MFMA peaks (MI355X_MICROARCH.md).  bf16x3 runs three bf16 MFMAs per
-# product (W_hi.X_hi + W_hi.X_lo + W_lo.X_hi), so its algorithmic ceiling is a third
-# of the bf16 peak.
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0, "bf16x3": 2500.0 / 3}
+# MI355X dense MFMA peaks (MI355X_MICROARCH.md).  bf16x3 / f16x3 run three 16-bit MFMAs
+# per product (W_hi.X_hi + W_hi.X_lo + W_lo.X_hi), so their algorithmic ceiling is a
+# third of the bf16 (= f16) peak.
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0, "bf16x3": 2500.0 / 3, "f16x3": 2500.0 / 3}
 METRIC = "rays/sec at 800x600x128spp (render_image, fine net, uniform samples)"
 GRID_RES = [(200, 150), (400, 300), (800, 600)]                 # reference main.py:134-141
 GRID_SPP = [32, 64, 128]
@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--precision", choices=["bf16", "fp32", "fp8", "bf16x3"], default="bf16")
+    ap.add_argument("--precision", choices=["bf16", "fp32", "fp8", "bf16x3", "f16x3"], default="bf16")
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--spp", type=int, default=128)
@@ -113,7 +113,8 @@ def check_gathered(r, pose, width, height, spp, rank, world):
     return {"gathered_equals_single": bool(torch.equal(frame[..., :3], rgb) and torch.equal(frame[..., 3], dep)),
             "rgb_max_abs": float((frame[..., :3] - rgb).abs().max()),
             "depth_max_abs": float((frame[..., 3] - dep).abs().max()),
-            "check": f"rank 0 rendered {width}x{height}x{spp} alone vs the {world} gathered band tiles"}
+            "check": f"rank 0 rendered {width}x{height}x{spp}" + (f"+{r.n_importance}" if r.n_importance else "")
+                     + f" ({r.precision}) alone vs the {world} gathered band tiles"}
 
 
 def dist_record():
@@ -247,7 +248,7 @@ def readme_grid(renderers, pose, rank, world):
         for (w, h) in GRID_RES:
             for spp in GRID_SPP:
                 step, band_rays = frame_step(r, pose, w, h, spp, rank, world)
-                n = 2 if prec in ("fp32", "bf16x3") and w * h * spp >= 400 * 300 * 128 else 4
+                n = 2 if prec in ("fp32", "bf16x3", "f16x3") and w * h * spp >= 400 * 300 * 128 else 4
                 dt = time_steps(step, 1, n, world)
                 kms = D.reduce_max(kernel_ms(r, n))
                 flop = w * h * spp * W.FLOPS_PER_SAMPLE
@@ -271,16 +272,30 @@ def other_configs(ckpt, pose, local, ref32):
     step, _ = frame_step(ref32, pose, 400, 300, 64, 0, 1)
     dt = time_steps(step, 1, 3, 1)
     out["c2_fp32_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt}
-    # C2 on the split-bf16 path, which is held to the same 1e-4 gate (tests/test_gpu_bf16x3.py)
-    x3 = MI355XRenderer("bf16x3", device_index=local)
+    # C2 and the headline frame on the split-fp16 path, the parity-grade fast path held to
+    # the same 1e-4 gate as fp32 on the Lego fixtures (tests/test_gpu_lego.py)
+    x3 = MI355XRenderer("f16x3", device_index=local)
     x3.setup(ckpt)
+    x3.hip.set_profiling(True)
     step, _ = frame_step(x3, pose, 400, 300, 64, 0, 1)
     dt = time_steps(step, 1, 3, 1)
+    out["c2_f16x3_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt}
+    step, _ = frame_step(x3, pose, 800, 600, 128, 0, 1)
+    dt = time_steps(step, 1, 4, 1)
+    ms = kernel_ms(x3, 4)
     rgb3, d3 = x3.render_rows(pose, (800, 600), 128, 292, 308)
     rgb32, d32 = ref32.render_rows(pose, (800, 600), 128, 292, 308)
-    out["c2_bf16x3_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt,
-                                   "rgb_max_abs_vs_fp32_800x600x128_band": float((rgb3 - rgb32).abs().max()),
-                                   "depth_max_abs_vs_fp32_800x600x128_band": float((d3 - d32).abs().max())}
+    flop = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE
+    out["gate_path_f16x3_800x600x128"] = {
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms,
+        "mlp_tflops": flop / (ms * 1e-3) / 1e12,
+        "frac_of_bf16_dense_peak": flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
+        "frac_of_x3_ceiling": flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"],
+        "rgb_max_abs_vs_fp32_band": float((rgb3 - rgb32).abs().max()),
+        "depth_max_abs_vs_fp32_band": float((d3 - d32).abs().max()),
+        "note": "the north star's two clauses side by side: this path meets the 1e-4 gate against the "
+                "reference on Lego (tests/test_gpu_lego.py) at three f16 MFMAs per product; the headline "
+                "bf16 line meets the roofline clause, not the gate"}
 
     h = MI355XRenderer("bf16", n_importance=128, device_index=local)
     h.setup(ckpt)
@@ -626,7 +641,8 @@ def main():
 
     flop_launch = band_rays * spp * W.FLOPS_PER_SAMPLE
     traffic, traffic_src = None, None
-    kname = f"mlp_{args.precision}_kernel"
+    kname = {"bf16x3": "mlp_x3_kernel<OpBf16>", "f16x3": "mlp_x3_kernel<OpF16>"}.get(args.precision,
+                                                                                    f"mlp_{args.precision}_kernel")
     pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
     if os.path.exists(pmc) and (width, height, spp, world) == (800, 600, 128, 1):
         # the headline launch's own counters: profiles/collect.sh profiles the
@@ -682,8 +698,8 @@ def main():
                 f8.setup(ckpt)
         f8.hip.set_profiling(True)
         rs = {"bf16": r if args.precision == "bf16" else None, "fp8": f8, "fp32": ref,
-              "bf16x3": r if args.precision == "bf16x3" else None}
-        for p in ("bf16", "bf16x3"):
+              "f16x3": r if args.precision == "f16x3" else None}
+        for p in ("bf16", "f16x3"):
             if rs[p] is None:
                 rs[p] = MI355XRenderer(p, device_index=local)
                 rs[p].setup(ckpt)

@@ -52,7 +52,7 @@ constexpr int kUnitB = 2 * kUnitBytes;                                // 4 KiB: 
 #define NERF_X3_SLOTS 3
 #endif
 #ifndef NERF_X3_PF
-#define NERF_X3_PF 2
+#define NERF_X3_PF 3
 #endif
 constexpr int kChunkUnits = NERF_X3_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitB;                         // 16 KiB
@@ -103,13 +103,23 @@ struct OpF16 {
   static __device__ __forceinline__ f32x16 mfma(const frag& a, const frag& b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
   }
-  // hi = f16(v) (v_cvt_pk_f16_f32, round to nearest even), lo = f16(v - hi) (exact
-  // difference; subnormal lo for |v| < 2^-3 keeps an absolute 2^-25)
+  // hi = f16(v) (v_cvt_pk_f16_f32, round to nearest even), lo = f16(v - hi): one
+  // v_fma_mix{lo,hi}_f16 per value computes fma(-f32(hi half), 1, v) -- the exact
+  // difference -- and rounds it to f16 into its half (subnormal lo for |v| < 2^-3
+  // keeps an absolute 2^-25); the compiler's form is two conversions back to f32,
+  // a packed subtraction and a second packed conversion
   static __device__ __forceinline__ void split_pair(float a, float b, unsigned& hi, unsigned& lo) {
-    const f16x2 h = __builtin_convertvector(f32x2{a, b}, f16x2);
-    const f32x2 hf = __builtin_convertvector(h, f32x2);
-    hi = __builtin_bit_cast(unsigned, h);
+    hi = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, f16x2));
+#ifdef NERF_X3_NO_MIX
+    const f32x2 hf = __builtin_convertvector(__builtin_bit_cast(f16x2, hi), f32x2);
     lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{__fsub_rn(a, hf[0]), __fsub_rn(b, hf[1])}, f16x2));
+#else
+    unsigned l;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(l) : "v"(hi), "v"(a), "v"(b));
+    lo = l;
+#endif
   }
 };
 
@@ -162,6 +172,9 @@ struct Ctx {
 };
 
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
+#ifdef NERF_X3_ABLATE_NODMA   // timing-only lab build (wrong results): the weight stream is not restaged
+  if (g >= kSlots) return;
+#endif
   char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i)
@@ -209,7 +222,9 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   const int g = (n + kPf) / kChunkUnits - 1;
   wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
+#ifndef NERF_X3_ABLATE_NOBARRIER   // timing-only lab build (wrong results): no seam barriers
   __builtin_amdgcn_s_barrier();
+#endif
   compiler_fence();
   stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
 }
@@ -219,6 +234,11 @@ NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) /
 NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
 template <class Op>
 __device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4& fhi, u32x4& flo) {
+#ifdef NERF_X3_ABLATE_NOCONV   // timing-only lab build (wrong results): accumulator bits as fragments
+  fhi[pr & 3] = __builtin_bit_cast(unsigned, tile[2 * pr]);
+  flo[pr & 3] = __builtin_bit_cast(unsigned, tile[2 * pr + 1]);
+  return;
+#endif
   unsigned h2, l2;
   Op::split_pair(relu(tile[2 * pr]), relu(tile[2 * pr + 1]), h2, l2);
   fhi[pr & 3] = h2;
@@ -464,18 +484,25 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
   wait_vmcnt(0);   // the stream ran into a tile that does not exist: let it land
 }
 
+// NERF_X3_LAB (timing builds of make variant_x3 only): instantiate just the f16
+// render-pass kernel, so a variant compiles in a fifth of the time.
 template <class Op>
 hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
                      bool explicit_points, hipStream_t stream, float* seg) {
+#ifdef NERF_X3_LAB
+  if (explicit_points || !__is_same(Op, OpF16)) return hipErrorNotSupported;
+#endif
   if (n_points <= 0) return hipSuccess;
   if (seg != nullptr && (explicit_points || src.n_samples % kSamplesPerWave != 0)) return hipErrorInvalidValue;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
+#ifndef NERF_X3_LAB
   if (explicit_points)
     hipLaunchKernelGGL((mlp_x3_kernel<true, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,
                        n_points, (f32x4*)out, (f32x4*)nullptr, X3TrainOut{});
   else
+#endif
     hipLaunchKernelGGL((mlp_x3_kernel<false, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,
                        n_points, (f32x4*)out, (f32x4*)seg, X3TrainOut{});
   return hipGetLastError();
@@ -485,7 +512,11 @@ hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src
 
 hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
                              bool explicit_points, hipStream_t stream, float* seg) {
+#ifdef NERF_X3_LAB
+  return hipErrorNotSupported;
+#else
   return launch_x3<OpBf16>(blob, params, src, n_points, out, explicit_points, stream, seg);
+#endif
 }
 
 hipError_t launch_mlp_f16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
@@ -495,6 +526,9 @@ hipError_t launch_mlp_f16x3(const void* blob, const float* params, const SampleS
 
 hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
                                    const X3TrainOut& o, hipStream_t stream) {
+#ifdef NERF_X3_LAB
+  return hipErrorNotSupported;
+#endif
   if (n_points <= 0) return hipSuccess;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU

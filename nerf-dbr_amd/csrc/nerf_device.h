@@ -37,12 +37,37 @@ __device__ __forceinline__ void sincos_fast(float a, float* s, float* c) {
   *c = __builtin_amdgcn_cosf(t);
 }
 
-// sin/cos of fl(2^k*pi)*x: accurate ocml sincosf (the fp32 parity path) or the
-// reduced-precision sincos_fast (the bf16 path).
+// sin and cos of an fp32 argument to within 1 ulp of torch's CPU sin/cos over the
+// encodings' arguments (|a| = |fl(2^k pi) x| < 2^15; measured on 60k arguments of
+// the reference's PositionalEncoding, tools/sincos_lab.py), for the fp32 and split
+// paths.  Cody-Waite reduction by pi/2 in three fp32 parts with FMA -- the first
+// step a - q*P1 is exact (a multiple of 2^-23 below 2 in magnitude) -- then
+// minimax polynomials on [-pi/4, pi/4] (sin to r^9, cos to r^10; fitted in
+// float64, rounded to fp32) and the quadrant's swap and signs.  About 20 VALU
+// per pair against ocml's sincosf, which also evaluates its large-argument
+// (Payne-Hanek) reduction for every lane.
+__device__ __forceinline__ void sincos_acc(float a, float* s, float* c) {
+  const float q = __builtin_rintf(__fmul_rn(a, 0x1.45f306p-1f));            // 2/pi
+  float r = fmaf(-q, 0x1.921fb6p+0f, a);                                   // pi/2 = P1 + P2 + P3
+  r = fmaf(-q, -0x1.777a5cp-25f, r);
+  r = fmaf(-q, -0x1.ee59dap-50f, r);
+  const float z = __fmul_rn(r, r);
+  const float ps = fmaf(fmaf(fmaf(0x1.6c99b0p-19f, z, -0x1.a00e8cp-13f), z, 0x1.111108p-7f), z, -0x1.555556p-3f);
+  const float sn = fmaf(__fmul_rn(r, z), ps, r);
+  const float pc = fmaf(fmaf(fmaf(-0x1.23f15cp-22f, z, 0x1.a00ffap-16f), z, -0x1.6c16b6p-10f), z, 0x1.555556p-5f);
+  const float cs = fmaf(__fmul_rn(z, z), pc, fmaf(-0.5f, z, 1.0f));
+  const int qi = int(q);
+  const float s0 = (qi & 1) ? cs : sn, c0 = (qi & 1) ? sn : cs;
+  *s = (qi & 2) ? -s0 : s0;
+  *c = ((qi + 1) & 2) ? -c0 : c0;
+}
+
+// sin/cos of fl(2^k*pi)*x: sincos_acc (the fp32 and split parity paths) or the
+// reduced-precision sincos_fast (the bf16 / fp8 paths).
 template <bool kFast>
 __device__ __forceinline__ void pe_sincos(float c, float x, float* s, float* co) {
   if (kFast) sincos_fast(__fmul_rn(c, x), s, co);
-  else sincosf(__fmul_rn(c, x), s, co);
+  else sincos_acc(__fmul_rn(c, x), s, co);
 }
 
 // Position encoding slots of lane half h (nerf_layout.h pe_slot_feature):

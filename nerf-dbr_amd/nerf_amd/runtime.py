@@ -357,7 +357,7 @@ class Device:
         _check(self.lib.nerf_ctx_set_profiling(self._ctx, 1 if enable else 0))
 
     def set_fused_composite(self, enable, coarse: bool = True) -> None:
-        """NERF_OPT_FUSED_COMPOSITE: compositing in the bf16/fp8 MLP epilogue (default on),
+        """NERF_OPT_FUSED_COMPOSITE: compositing in the bf16 / fp8 / split MLP epilogue (default on),
         for the rendered pass and (``coarse``) the hierarchical coarse pass's weights."""
         _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_FUSED_COMPOSITE,
                                             (1 if enable else 0) | (2 if enable and coarse else 0)))

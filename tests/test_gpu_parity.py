@@ -120,7 +120,9 @@ def test_render_bf16_error_bounded(r16, golden):
         rgb, depth = r16.render_image(torch.from_numpy(g["poses"][k]), (200, 150), 32)
         er, ed = maxabs(rgb, g[f"rgb_{k}"]), maxabs(depth, g[f"depth_{k}"])
         print(f"bf16 200x150x32 view {k}: rgb {er:.3e} depth {ed:.3e}")
-        assert er < 0.1 and ed < 0.5
+        # measured (round 3): rgb 1.6-2.2e-3, depth 4.7-8.7e-3 -- the per-sample kernel is
+        # pinned to its MFMA-order restatement in test_gpu_restated.py; this bounds the image
+        assert er < 5e-3 and ed < 2.5e-2
 
 
 def test_importance_sampler_matches_oracle(r32):
@@ -347,7 +349,7 @@ def test_render_fp8_error_vs_fp32(r8, r32, golden):
     mr = float((rgb8 - rgb32).abs().mean())
     print(f"fp8 vs fp32 800x600x128 band: rgb max {er:.3e} mean {mr:.3e}, depth max {ed:.3e}")
     assert torch.isfinite(rgb8).all() and torch.isfinite(d8).all()
-    assert er < 0.1 and mr < 0.01
+    assert er < 5e-2 and mr < 1e-2           # measured (round 3): rgb max 1.4e-2, mean 3.2e-3
 
 
 def test_fp8_error_below_reference_compressed(r8, r32):
@@ -643,8 +645,8 @@ def test_importance_sampler_exact_paths(r32, s, kind):
 def test_ragged_shapes_reduced_precision(ckpt, r32, precision, res, s):
     """Partial 256-sample tiles and partial 32-sample segments on the bf16 / fp8
     MLPs (fused compositing when S % 32 == 0, the sequential path otherwise),
-    against the fp32 parity path on the same pose, with the tolerances of the
-    full-size tests (test_render_bf16_error_bounded, test_render_fp8_error_vs_fp32)."""
+    against the fp32 parity path on the same pose, bounded at about three times the
+    measured error of each path."""
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
 
     r = MI355XRenderer(precision)
@@ -657,11 +659,14 @@ def test_ragged_shapes_reduced_precision(ckpt, r32, precision, res, s):
     er, ed = maxabs(rgb, rgb32.cpu().numpy()), maxabs(depth, d32.cpu().numpy())
     mr = float((rgb.cpu() - rgb32.cpu()).abs().mean())
     print(f"{precision} {res}x{s}: rgb max {er:.3e} mean {mr:.3e}, depth max {ed:.3e}")
-    assert er < 0.1 and ed < 0.5 and mr < 0.01
+    # measured (round 3): bf16 rgb <= 1.4e-3, depth <= 1.7e-3; fp8 rgb <= 1.4e-2, depth <= 2.9e-2
+    tol_rgb, tol_depth, tol_mean = (5e-3, 1e-2, 1e-3) if precision == "bf16" else (5e-2, 0.1, 1.5e-2)
+    assert er < tol_rgb and ed < tol_depth and mr < tol_mean
 
 
 @pytest.mark.parametrize("precision,spp,n_imp", [("fp32", 32, 0), ("bf16", 128, 0), ("bf16", 64, 128),
-                                                 ("fp8", 64, 0), ("bf16", 48, 0)])
+                                                 ("fp8", 64, 0), ("bf16", 48, 0), ("f16x3", 128, 0),
+                                                 ("bf16x3", 64, 64), ("f16x3", 48, 0)])
 def test_render_band_packed_matches_render_rows(ckpt, precision, spp, n_imp):
     """nerf_render_band (the multi-GPU path's packed [rows, W, 4] tile) holds exactly
     render_rows' rgb and depth, for fused and sequential compositing and the

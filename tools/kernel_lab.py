@@ -67,8 +67,9 @@ def main():
     ap.add_argument("--precision", choices=sorted(rt.PRECISIONS), default="bf16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--spp", type=int, default=128)
+    ap.add_argument("--ckpt", choices=["lego", "synthetic"], default="lego")
     args = ap.parse_args()
-    _, fine = W.synthetic_models(0)
+    _, fine = W.lego_models() if args.ckpt == "lego" else W.synthetic_models(0)
     libs = [Lib(p, fine, rt.PRECISIONS[args.precision]) for p in args.libs]
     pose = np.eye(4, dtype=np.float32)
     pose[2, 3] = 4.0
