@@ -62,11 +62,14 @@ __device__ __forceinline__ void sincos_acc(float a, float* s, float* c) {
   *c = ((qi + 1) & 2) ? -c0 : c0;
 }
 
-// sin/cos of fl(2^k*pi)*x: sincos_acc (the fp32 and split parity paths) or the
-// reduced-precision sincos_fast (the bf16 / fp8 paths).
-template <bool kFast>
+// sin/cos of fl(2^k*pi)*x: sincos_acc (the fp32 and split parity paths), the
+// reduced-precision sincos_fast (the bf16 / fp8 paths), or ocml's sincosf (kOcml: the
+// training kernels, whose gradient parity tests sit at the ReLU-flip floor measured
+// with it; both are within an ulp or two of torch).
+template <bool kFast, bool kOcml = false>
 __device__ __forceinline__ void pe_sincos(float c, float x, float* s, float* co) {
   if (kFast) sincos_fast(__fmul_rn(c, x), s, co);
+  else if (kOcml) sincosf(__fmul_rn(c, x), s, co);
   else sincos_acc(__fmul_rn(c, x), s, co);
 }
 
@@ -88,7 +91,7 @@ __device__ __forceinline__ void sincos_doubling(float c0, float x, float* s, flo
   }
 }
 
-template <bool kFast = false>
+template <bool kFast = false, bool kOcml = false>
 __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, float (&pe)[32]) {
   const float xs[3] = {x0, x1, x2};
   if (kFast) {
@@ -109,7 +112,7 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
         float s, co;
-        pe_sincos<false>(c, xs[m], &s, &co);
+        pe_sincos<false, kOcml>(c, xs[m], &s, &co);
         pe[6 * kk + m] = s;
         pe[6 * kk + 3 + m] = co;
       }
@@ -119,7 +122,7 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
   pe[31] = h ? 0.0f : x1;
 }
 
-template <bool kFast = false>
+template <bool kFast = false, bool kOcml = false>
 __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, float (&de)[16]) {
   const float ds[3] = {d0, d1, d2};
   if (kFast) {
@@ -140,7 +143,7 @@ __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, 
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
         float s, co;
-        pe_sincos<false>(c, ds[m], &s, &co);
+        pe_sincos<false, kOcml>(c, ds[m], &s, &co);
         de[6 * kk + m] = s;
         de[6 * kk + 3 + m] = co;
       }

@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void train_encode_kernel(const float* __restri
 #pragma unroll
   for (int k = 0; k < 10; ++k)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) pe_sincos<false>(pe_coef(k), x[c], &v[3 + 6 * k + c], &v[6 + 6 * k + c]);
+    for (int c = 0; c < 3; ++c) pe_sincos<false, true>(pe_coef(k), x[c], &v[3 + 6 * k + c], &v[6 + 6 * k + c]);
   v[63] = 0.0f;
   f32x4* po = (f32x4*)(pe + p * kPeLd);
 #pragma unroll
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void train_encode_kernel(const float* __restri
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) pe_sincos<false>(pe_coef(k), d[c], &u[3 + 6 * k + c], &u[6 + 6 * k + c]);
+    for (int c = 0; c < 3; ++c) pe_sincos<false, true>(pe_coef(k), d[c], &u[3 + 6 * k + c], &u[6 + 6 * k + c]);
   u[27] = 0.0f;
   f32x4* du = (f32x4*)(dpe + p * kDpeLd);
 #pragma unroll

@@ -24,11 +24,22 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def kernel_key(name: str) -> str:
+    """Short kernel names: the split kernels are one template (mlp_x3.h), told apart by
+    their operand type (bench.py's roofline.kernel uses the same keys)."""
+    if "mlp_x3_kernel" in name:
+        return "mlp_x3_kernel<OpF16>" if "OpF16" in name else "mlp_x3_kernel<OpBf16>"
+    for k in ("mlp_bf16_kernel", "mlp_fp8_kernel", "mlp_f32_kernel"):
+        if k in name:
+            return k
+    return name
+
+
 def per_kernel(path, counter):
     acc = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            acc.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+            acc.setdefault(kernel_key(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
@@ -36,7 +47,7 @@ def main(src: str, dest: str) -> None:
     os.makedirs(dest, exist_ok=True)
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-        stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+        stats[kernel_key(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                             "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6,
                             "pct": float(r["Percentage"])}
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")

@@ -30,7 +30,8 @@ def main(src, dest, prec):
          "lds_bank_conflict_cycles": cnt["SQ_LDS_BANK_CONFLICT"]}
     summ = os.path.join(dest, "summary.json")
     if os.path.exists(summ):
-        k = json.load(open(summ))["kernels"].get(f"mlp_{prec}_kernel")
+        key = {"f16x3": "mlp_x3_kernel<OpF16>", "bf16x3": "mlp_x3_kernel<OpBf16>"}.get(prec, f"mlp_{prec}_kernel")
+        k = json.load(open(summ))["kernels"].get(key)
         if k:
             d["effective_clock_ghz"] = cycles_xcd / (k["avg_ms"] * 1e-3) / 1e9
     os.makedirs(dest, exist_ok=True)
