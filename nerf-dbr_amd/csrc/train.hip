@@ -765,8 +765,8 @@ __global__ __launch_bounds__(256, 1) void train_fwd_kernel(const f32x4* __restri
   float x[3], d[3];
   fetch_sample<false>(src, pc, x, d);
   float pe[32], de[16];
-  pos_encode(x[0], x[1], x[2], h, pe);
-  dir_encode(d[0], d[1], d[2], h, de);
+  pos_encode<false, true>(x[0], x[1], x[2], h, pe);
+  dir_encode<false, true>(d[0], d[1], d[2], h, de);
   f32x16 a[8], b[8];
   // each layer's ReLU, bit words and rows happen while the next layer runs (fwd_layer)
   float* const nul = nullptr;

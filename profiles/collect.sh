@@ -17,7 +17,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--precision $PREC --cpu-seconds 0 --no-error-check --no-extras"
+ARGS="--precision $PREC --cpu-seconds 0 --no-error-check --no-extras --no-train"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run \
   -- python3 $ROOT/bench.py --steps 10 --warmup 3 $ARGS > "$OUT/bench_under_rocprof.json" 2> "$OUT/trace.log" || exit $?
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT/pmc_fetch" -o run \
