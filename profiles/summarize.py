@@ -24,11 +24,16 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+PRECISION = None      # the profiled command's --precision (set in main)
+
+
 def kernel_key(name: str) -> str:
-    """Short kernel names: the split kernels are one template (mlp_x3.h), told apart by
-    their operand type (bench.py's roofline.kernel uses the same keys)."""
+    """Short kernel names: the split kernels are one template (mlp_x3.h) that rocprofv3
+    names `mlp_x3_kernel` either way; the profiled command's precision tells them apart
+    (bench.py's roofline.kernel uses the same keys)."""
     if "mlp_x3_kernel" in name:
-        return "mlp_x3_kernel<OpF16>" if "OpF16" in name else "mlp_x3_kernel<OpBf16>"
+        f16 = "OpF16" in name or ("OpBf16" not in name and PRECISION == "f16x3")
+        return "mlp_x3_kernel<OpF16>" if f16 else "mlp_x3_kernel<OpBf16>"
     for k in ("mlp_bf16_kernel", "mlp_fp8_kernel", "mlp_f32_kernel"):
         if k in name:
             return k
@@ -44,7 +49,10 @@ def per_kernel(path, counter):
 
 
 def main(src: str, dest: str) -> None:
+    global PRECISION
     os.makedirs(dest, exist_ok=True)
+    words = open(os.path.join(src, "command.txt")).read().split()
+    PRECISION = words[words.index("--precision") + 1] if "--precision" in words else None
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
         stats[kernel_key(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
