@@ -5,7 +5,7 @@
  * given as 22 raw little-endian fp32 tensors in state-dict order (the layout
  * NERF_N_PARAMS documents), and writes RGB and depth as raw fp32.
  *
- *   render_c <params.bin> <width> <height> <spp> <precision 0|1|2|3> <out.bin> [t.bin]
+ *   render_c <params.bin> <width> <height> <spp> <precision 0|1|2|3|4> <out.bin> [t.bin]
  *
  * t.bin (optional): the spp fp32 values of torch.linspace(0, 1, spp), for bit
  * parity with the Python host; otherwise the table is computed here.

@@ -160,3 +160,51 @@ def test_lego_throughput_paths_error_vs_fp32(ckpt, golden, precision, tol_rgb_me
         print(f"lego {precision} 200x150x32 view {int(g['pose_ids'][k])}: rgb max {er:.3e} mean {mr:.3e} "
               f"depth max {ed:.3e}")
         assert torch.isfinite(rgb).all() and mr < tol_rgb_mean and er < 1.0
+
+
+@pytest.mark.parametrize("precision", GATE)
+def test_lego_stratified_hierarchical_chain_at_gate(ckpt, precision):
+    """Stratified coarse samples (injected t_rand, rendering.py:42-47) and per-ray
+    importance draws (injected u) on Lego: GPU coarse weights -> oracle sampler == the
+    render's fine z -> oracle fine pass within 1e-4 of the render."""
+    from oracle import nerf_oracle as O
+
+    nc, ni = 32, 64
+    r = renderer(ckpt, precision, n_importance=ni)
+    _, f = W.lego_models()
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][0])
+    w, h = 32, 24
+    gen = torch.Generator().manual_seed(5)
+    t_rand = torch.rand(w * h, nc, generator=gen)
+    u = torch.sort(torch.rand(w * h, ni, generator=gen), -1).values
+    rgb, depth = [t.clone() for t in r.render_rows(pose, (w, h), nc, 0, h, t_rand=t_rand, u=u)]
+    zf_render = torch.empty(w * h, nc + ni, dtype=torch.float32, device="cuda")
+    r.hip.last_fine_z(w * h, nc + ni, zf_render)
+    o, d = O.generate_rays(pose, w, h)
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    zc = O.stratified_z(O.uniform_z(nc), t_rand).contiguous()
+    _, _, _, w_gpu = r.render_rays_z(o, d, zc, use_fine=False, with_weights=True)
+    zf = O.fine_z(zc, w_gpu.cpu(), u)
+    assert torch.equal(zf, zf_render.cpu())
+    pts = O.sample_points(o, d, zf)
+    s_, c_ = O.nerf_forward(O.Net(f), pts.reshape(-1, 3), d[:, None].expand_as(pts).reshape(-1, 3))
+    ref_rgb, ref_dep = O.composite(s_.reshape(w * h, -1, 1), c_.reshape(w * h, -1, 3), zf, d)
+    er, ed = maxabs(rgb.reshape(-1, 3), ref_rgb), maxabs(depth.reshape(-1), ref_dep)
+    print(f"lego {precision} stratified hierarchical {w}x{h} {nc}+{ni}: rgb {er:.3e} depth {ed:.3e}")
+    assert er < TOL_RENDER and ed < TOL_RENDER
+
+
+@pytest.mark.parametrize("res,s", [((1, 1), 1), ((7, 3), 2), ((33, 9), 100), ((131, 3), 32)])
+def test_lego_f16x3_edge_shapes_vs_oracle(ckpt, res, s):
+    """Partial tiles and segments, S not a multiple of 32 (sequential composite) and of 32
+    (fused), on real content, against the oracle's fp32 render."""
+    from oracle import nerf_oracle as O
+
+    _, f = W.lego_models()
+    r = renderer(ckpt, "f16x3")
+    pose = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays.npz"))["poses"][2])
+    rgb, depth = r.render_image(pose, res, s)
+    ref_rgb, ref_depth = O.render_image(O.Net(f), pose, res, s)
+    er, ed = maxabs(rgb, ref_rgb), maxabs(depth, ref_depth)
+    print(f"lego f16x3 {res}x{s}: rgb {er:.3e} depth {ed:.3e}")
+    assert er < TOL_RENDER and ed < TOL_RENDER

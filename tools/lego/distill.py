@@ -207,7 +207,7 @@ def loss_fn(student, o, d, z, st, ct):
 
 def train(which, steps, rays, seed, budget_s, log, dev, init=None, lr0=5e-4, lr1=2.5e-5):
     """Adam with the rate decayed exponentially 5e-4 -> 2.5e-5 over the run; the run is
-    ``steps`` long, or shorter when the first 30 steps' pace says ``budget_s`` seconds
+    ``steps`` long, or shorter when the pace of steps 20-60 says ``budget_s`` seconds
     would not cover it (the decay is then re-spread over the steps that fit)."""
     teacher = load_teacher(which, dev)
     torch.manual_seed(seed)
@@ -224,10 +224,15 @@ def train(which, steps, rays, seed, budget_s, log, dev, init=None, lr0=5e-4, lr1
     last = t0
     it = 0
     while it < steps:
-        if it == 30:
-            torch.cuda.synchronize(dev) if dev.type == "cuda" else None
-            pace = (time.time() - t0) / 30
-            steps = max(31, min(steps, int(budget_s / pace)))
+        if it == 20:                           # pace from steps 20..60 (the first ones warm up)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t20 = time.time()
+        if it == 60:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            pace = (time.time() - t20) / 40
+            steps = max(61, min(steps, 60 + int((budget_s - (time.time() - t0)) / pace)))
             log(f"[{which}] {1e3 * pace:.1f} ms/step -> {steps} steps")
         lr = lr0 * (lr1 / lr0) ** (it / max(1, steps - 1))
         for grp in opt.param_groups:
