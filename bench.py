@@ -261,6 +261,18 @@ def readme_grid(renderers, pose, rank, world):
     return out
 
 
+def band_nan(r, pose, rows=(292, 308)):
+    """Rows [292, 308) of the 800x600x128 frame into NaN-filled outputs (a render that did
+    not write shows as NaN in the error fields instead of stale memory)."""
+    import torch
+
+    rgb = torch.full((rows[1] - rows[0], 800, 3), float("nan"), device=r.torch_device())
+    dep = torch.full((rows[1] - rows[0], 800), float("nan"), device=r.torch_device())
+    r.render_rows(pose, (800, 600), 128, rows[0], rows[1], rgb, dep)
+    torch.cuda.synchronize()
+    return rgb, dep
+
+
 def other_configs(ckpt, pose, local, ref32):
     """The BASELINE configs besides the headline, 1 GPU each:
     C2 400x300x64 fp32 (the parity path), C3 800x600 64+128 hierarchical bf16,
@@ -283,8 +295,8 @@ def other_configs(ckpt, pose, local, ref32):
     step, _ = frame_step(x3, pose, 800, 600, 128, 0, 1)
     dt = time_steps(step, 1, 4, 1)
     ms = kernel_ms(x3, 4)
-    rgb3, d3 = x3.render_rows(pose, (800, 600), 128, 292, 308)
-    rgb32, d32 = ref32.render_rows(pose, (800, 600), 128, 292, 308)
+    rgb3, d3 = band_nan(x3, pose)
+    rgb32, d32 = band_nan(ref32, pose)
     flop = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE
     out["gate_path_f16x3_800x600x128"] = {
         "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms,
@@ -317,8 +329,8 @@ def other_configs(ckpt, pose, local, ref32):
     dt = time_steps(step, 2, 5, 1)
     ms = kernel_ms(f8, 5)
     tf = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE / (ms * 1e-3) / 1e12
-    rgb8, d8 = f8.render_rows(pose, (800, 600), 128, 292, 308)
-    rgb32, d32 = ref32.render_rows(pose, (800, 600), 128, 292, 308)
+    rgb8, d8 = band_nan(f8, pose)
+    rgb32, d32 = band_nan(ref32, pose)
     out["c5_fp8_800x600x128"] = {
         "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms, "mlp_tflops": tf,
         "mlp_frac_fp8_peak": tf / PEAK_TFLOPS["fp8"],
@@ -682,8 +694,12 @@ def main():
     if rank == 0 and args.precision != "fp32" and not args.no_error_check:
         # bf16 / fp8 vs the fp32 path (itself gated at 1e-4 vs the reference in tests/) on a band
         a0, a1 = height // 2 - 8, height // 2 + 8
-        rgb32, d32 = ref.render_rows(pose, (width, height), spp, a0, a1)
-        rgb_lp, d_lp = r.render_rows(pose, (width, height), spp, a0, a1)
+        rgb32 = torch.full((a1 - a0, width, 3), float("nan"), device=r.torch_device())
+        d32 = torch.full((a1 - a0, width), float("nan"), device=r.torch_device())
+        rgb_lp, d_lp = torch.full_like(rgb32, float("nan")), torch.full_like(d32, float("nan"))
+        ref.render_rows(pose, (width, height), spp, a0, a1, rgb32, d32)
+        r.render_rows(pose, (width, height), spp, a0, a1, rgb_lp, d_lp)
+        torch.cuda.synchronize()
         extra[f"{args.precision}_vs_fp32_rgb_max_abs"] = float((rgb_lp - rgb32).abs().max())
         extra[f"{args.precision}_vs_fp32_rgb_mean_abs"] = float((rgb_lp - rgb32).abs().mean())
         extra[f"{args.precision}_vs_fp32_depth_max_abs"] = float((d_lp - d32).abs().max())
