@@ -322,6 +322,20 @@ def other_configs(ckpt, pose, local, ref32):
         "mlp_tflops": flop / (mlp_ms * 1e-3) / 1e12, "mlp_frac_bf16_peak": flop / (mlp_ms * 1e-3) / 1e12 / 2500.0,
         "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)"}
 
+    # C3 on the gate-passing path (split fp16 for both nets; the hierarchical chain is
+    # checked at the 1e-4 gate on Lego in tests/test_gpu_lego.py)
+    h3 = MI355XRenderer("f16x3", n_importance=128, device_index=local)
+    h3.setup(ckpt)
+    h3.hip.set_profiling(True)
+    step, _ = frame_step(h3, pose, 800, 600, 64, 0, 1)
+    dt = time_steps(step, 1, 2, 1)
+    st = h3.hip.stage_ms()
+    mlp_ms = st["coarse_mlp"] + st["fine_mlp"]
+    out["c3_hierarchical_f16x3_800x600_64+128"] = {
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms": st,
+        "mlp_tflops": flop / (mlp_ms * 1e-3) / 1e12, "mlp_frac_x3_ceiling": flop / (mlp_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"]}
+    del h3
+
     f8 = MI355XRenderer("fp8", device_index=local)
     f8.setup(ckpt)
     f8.hip.set_profiling(True)

@@ -172,15 +172,18 @@ struct Ctx {
   unsigned ring_addr, pe_addr, de_addr, bias_addr, ring_hi_addr;
 };
 
-__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
+__device__ __forceinline__ void stage_piece(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane,
+                                            int i) {
 #ifdef NERF_X3_ABLATE_NODMA   // timing-only lab build (wrong results): the weight stream is not restaged
   if (g >= kSlots) return;
 #endif
   char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
+  lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
+               lds_addr(dst + i * kThreads * 16));
+}
+__device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
 #pragma unroll
-  for (int i = 0; i < kGldsPerStage; ++i)
-    lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
-                 lds_addr(dst + i * kThreads * 16));
+  for (int i = 0; i < kGldsPerStage; ++i) stage_piece(blob, g, lds, wave_u, lane, i);
 }
 
 template <class Op>
@@ -218,8 +221,23 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, F (&ra)[kRing][4
 
 constexpr int kDmaOutstandingAtSeam = kSlots - 3;
 constexpr int kStageAhead = kSlots - 1;
+// NERF_X3_SPREAD (lab knob): a seam stages only its first LDS-DMA piece and the next
+// units one piece each, instead of all pieces back to back at the seam.
+#ifndef NERF_X3_SPREAD
+#define NERF_X3_SPREAD 0
+#endif
+static_assert(!NERF_X3_SPREAD || (kGldsPerStage <= kChunkUnits && kSlots >= 4),
+              "spread pieces land within a chunk, and need one chunk of slack at the next seam");
+NL_HD bool is_seam(int n) { return (n + kPf) % kChunkUnits == 0 && n + kPf < kUnits && n + kPf != 0; }
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
-  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
+  if (NERF_X3_SPREAD) {
+#pragma unroll
+    for (int i = 1; i < kGldsPerStage; ++i)
+      if (n - i >= 0 && is_seam(n - i))
+        stage_piece(cx.blob, ((n - i + kPf) / kChunkUnits - 1 + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u,
+                    cx.lane, i);
+  }
+  if (!is_seam(n)) return;
   const int g = (n + kPf) / kChunkUnits - 1;
   wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
@@ -227,7 +245,8 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   __builtin_amdgcn_s_barrier();
 #endif
   compiler_fence();
-  stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
+  if (NERF_X3_SPREAD) stage_piece(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane, 0);
+  else stage_chunk(cx.blob, (g + kStageAhead) % kTotalChunks, cx.lds, cx.wave_u, cx.lane);
 }
 
 // Conversion schedule of mlp_bf16.hip: one dword (two values) per unit.
