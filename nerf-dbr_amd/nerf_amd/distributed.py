@@ -128,9 +128,10 @@ def gather_bands(rgb_band, depth_band, width: int, height: int, group=None):
 
 def init_from_env():
     """(rank, world, local, device index) from torchrun's environment; joins the
-    process group when world > 1.  Backend RCCL ("nccl") unless NERF_DIST_BACKEND
-    says otherwise (gloo: the one-device rehearsal, ranks sharing device
-    local % device_count)."""
+    process group when world > 1, or at world 1 when NERF_DIST_FORCE_GROUP=1 (the
+    RCCL check on a one-GPU box: tests/test_gpu_parity.py).  Backend RCCL ("nccl")
+    unless NERF_DIST_BACKEND says otherwise (gloo: the one-device rehearsal, ranks
+    sharing device local % device_count)."""
     import os
 
     import torch
@@ -141,7 +142,7 @@ def init_from_env():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or os.environ.get("NERF_DIST_FORCE_GROUP") == "1":
         backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
@@ -215,7 +216,7 @@ def train_step_sharded(trainer, batch, select, t_rand, group=None):
     a, b = band(rank, world, n)
     grads = trainer.grad_tensor()
     loss = trainer.backward(batch, select[a:b], t_rand[a:b], n_rays_total=n)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(grads, group=group)
         dist.all_reduce(loss, group=group)
     trainer.update()

@@ -4,8 +4,11 @@ Every rank renders its row band (nerf_amd.distributed.band); the bands are
 all-gathered, and, separately, rendered as packed tiles and gathered to rank 0.
 Rank 0 compares both frames with a single-call full-frame render (bit-identical
 expected: rays are independent) and prints one JSON line.
-Backend from NERF_DIST_BACKEND (the test uses gloo so that two ranks can share
-one device; the 8-GPU bench uses RCCL).
+Backend from NERF_DIST_BACKEND (the two-rank test uses gloo so that two ranks can
+share one device; the 8-GPU bench uses RCCL).  With NERF_DIST_FORCE_GROUP=1 and one
+rank the same code runs over an RCCL process group of world size 1 (the one-GPU
+box's check of the nccl branches), plus an RCCL all-reduce of a gradient-store-
+sized device tensor.  Every rank prints one JSON line.
 """
 import json
 import os
@@ -40,7 +43,16 @@ def main():
                   and torch.equal(root[0], ref_rgb) and torch.equal(root[1], ref_depth))
     else:
         ok = root is None
-        print(json.dumps({"world": world, "bands": D.bands(world, h), "identical": ok}), flush=True)
+    rec = {"world": world, "rank": rank, "backend": dist.get_backend(), "bands": D.bands(world, h), "identical": ok}
+    if dist.get_backend() == "nccl":
+        # the training step's exchange: one all-reduce (SUM) of the 2 x 530,052-float gradient store
+        g = torch.arange(2 * 530_052, dtype=torch.float32, device="cuda") * (rank + 1)
+        dist.all_reduce(g)
+        want = torch.arange(2 * 530_052, dtype=torch.float32, device="cuda") * (world * (world + 1) // 2)
+        rec["all_reduce_ok"] = bool(torch.equal(g, want))
+        rec["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        ok = ok and rec["all_reduce_ok"]
+    print(json.dumps(rec), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     return 0 if ok else 1

@@ -399,7 +399,7 @@ def test_plain_c_host_matches_python(r32, tmp_path):
     assert np.array_equal(out[w * h * 3:], depth.cpu().numpy().ravel())
 
 
-def _torchrun(args, env_extra, timeout=300):
+def _torchrun(args, env_extra, timeout=300, nproc=2):
     import socket
     import subprocess
     import sys
@@ -408,7 +408,7 @@ def _torchrun(args, env_extra, timeout=300):
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     env = dict(os.environ, **env_extra)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
 
@@ -422,9 +422,8 @@ def test_multi_rank_rehearsal_on_one_device():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = _torchrun([os.path.join(repo, "tests", "dist_render_check.py")], {"NERF_DIST_BACKEND": "gloo"})
     assert res.returncode == 0, res.stderr[-3000:]
-    line = [l for l in res.stdout.splitlines() if l.startswith("{")][-1]
-    out = js.loads(line)
-    assert out["world"] == 2 and out["identical"]
+    lines = [js.loads(l) for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 2 and all(o["world"] == 2 and o["backend"] == "gloo" and o["identical"] for o in lines)
     res = _torchrun([os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--width", "200",
                      "--height", "150", "--spp", "32", "--cpu-seconds", "0", "--no-error-check"],
                     {"NERF_DIST_BACKEND": "gloo"})
@@ -440,6 +439,23 @@ def test_multi_rank_rehearsal_on_one_device():
     t = b["training"]                                 # data-parallel training step, every rank taking part
     assert t["n_gpus"] == 2 and t["rays_per_s"] > 0 and t["parallelism"].startswith("data parallel x2")
     assert t["loss_first_last"][-1] < t["loss_first_last"][0]
+
+
+@pytest.mark.parametrize("precision", ["bf16", "f16x3"])
+def test_rccl_process_group_world1(precision):
+    """The nccl branches of nerf_amd.distributed on this one-GPU box: an RCCL process
+    group of world size 1 (init_from_env with device_id), the band all-gather, the
+    packed-tile gather to the root and the gradient all-reduce, each through RCCL on
+    device tensors, the frames bit-identical to a single-call render."""
+    import json as js
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = _torchrun([os.path.join(repo, "tests", "dist_render_check.py")],
+                    {"NERF_DIST_FORCE_GROUP": "1", "NERF_DIST_BACKEND": "nccl", "NERF_CHECK_PRECISION": precision},
+                    nproc=1)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = js.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["world"] == 1 and out["backend"] == "nccl" and out["identical"] and out["all_reduce_ok"]
 
 
 def test_bench_single_gpu_json_contract():
