@@ -41,7 +41,7 @@ enum nerf_precision {
   NERF_FP32 = 0, /* f32-in MFMA (v_mfma_f32_32x32x2_f32); the parity path   */
   NERF_BF16 = 1, /* bf16-in MFMA (v_mfma_f32_32x32x16_bf16), f32 accumulate */
   NERF_FP8 = 2,  /* e4m3 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4): per-row weight
-                    scales, per-sample activation scales, f32 accumulate; the
+                    scales, activations e4m3 at scale 1 saturated at 448, f32 accumulate; the
                     compressed-weights path (config 5; the reference's int8
                     CompressedNeRFRenderer, src/benchmark/compressed_renderer.py) */
   NERF_BF16X3 = 3, /* split bf16 on the bf16 MFMA: W.X ~ Wh.Xh + Wh.Xl + Wl.Xh with

@@ -468,9 +468,8 @@ def bf16_mlp_restated(sd, pe, dpe):
 # defined here, as the kernel computes it (mlp_fp8.hip), in float64:
 #   * weights: e4m3 (RNE) of W / 2^e_r, e_r the smallest power of two with
 #     max|W_r| / 2^e_r <= 448, per output row r;
-#   * activations (previous layer's ReLU output): e4m3 of x / 2^e, one e per
-#     sample per 64-row block (rows 64v..64v+63 are the next layer's k-step v),
-#     e = frexp exponent of the block's largest value - 8 (range [128, 256));
+#   * activations (previous layer's ReLU output): e4m3 at scale 1 of the ReLU'd
+#     value saturated at 448 (v_med3_f32(x, 0, 448), then the RNE conversion);
 #   * encodings: e4m3 at scale 1; bias and accumulation in full precision;
 #   * heads (nerf_layout.h kFp8HeadUnits): density as one more fp8 row over C0's
 #     quantised input (its own row scale), colour in bf16 (weights and ReLU'd
@@ -488,13 +487,10 @@ def bf16_round(x):
     return t.float().numpy().astype(np.float64)
 
 
-def fp8_activation_exponent(x):
-    """x [rows, n] (rows a multiple of 64) -> per-row exponents [rows, n]: each
-    64-row block of a sample shares its block's scale (mlp_fp8.hip layer_fp8b)."""
-    rows, n = x.shape
-    m = np.maximum(x, 0).reshape(rows // 64, 64, n).max(axis=1)
-    e = np.frexp(m.astype(np.float32))[1].astype(np.int64) - 8
-    return np.repeat(e, 64, axis=0)
+def fp8_activation_round(x):
+    """ReLU'd fp32 activations as the next layer's e4m3 operands (mlp_fp8.hip
+    convert_tile): min(max(x, 0), 448), then e4m3 RNE, at scale 1."""
+    return e4m3_round(np.clip(x, 0.0, 448.0))
 
 
 def fp8_weight_rows(w, with_exp=False):
@@ -512,8 +508,7 @@ def fp8_mlp_restated(sd, pe, dpe, chain=True):
     Each Linear is an fp32 accumulation chain over its 64-wide MFMA k-steps, the
     products cut per group of 8 as the instruction does (MFMA_FP8_MODEL)."""
     def aq(x):
-        e = fp8_activation_exponent(x)
-        return e4m3_round(np.maximum(x, 0) / np.ldexp(1.0, e)) * np.ldexp(1.0, e), e
+        return fp8_activation_round(x), np.zeros(x.shape)
 
     pq, dq = e4m3_round(pe), e4m3_round(dpe)
     zp, zd = np.zeros(pq.shape), np.zeros(dq.shape)

@@ -303,8 +303,7 @@ def emulate_fp8(blob, prm, pe, dpe):
         a = e4m3_decode(raw).reshape(nq, ku, 2, 2, 64, 16)            # [q][u][o2][p][lane][16]
         a = a.transpose(0, 1, 2, 4, 3, 5).reshape(nq, ku, 2, 64, 32)   # [q][u][o2][lane][byte j]
         if x is not None:
-            e = O.fp8_activation_exponent(x)
-            xq = e4m3_round(np.maximum(x, 0) / np.ldexp(1.0, e)) * np.ldexp(1.0, e)
+            xq = O.fp8_activation_round(x)
         if extra:
             feats, fn, used = (pe, pe_slot_feature, 32) if extra == "pos" else (dpe, dpe_slot_feature, 16)
             ext = [e4m3_round(np.stack([feats[fn(h, j)] if (j < used and fn(h, j) >= 0) else np.zeros(n)
