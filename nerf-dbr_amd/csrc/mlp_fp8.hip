@@ -72,8 +72,11 @@ constexpr int kSlots = NERF_FP8_SLOTS;
 // bit-identical output; a 5-slot ring (restoring the staging distance) was
 // slower (-1.1 %).  Timing ablations and other lab variants of round 1
 //  are not part of this source.
-constexpr int kLagOn = 1;
-static_assert(kSlots >= 4, "a lagged ring needs 4 slots");
+#ifndef NERF_FP8_LAG
+#define NERF_FP8_LAG 1
+#endif
+constexpr int kLagOn = NERF_FP8_LAG;
+static_assert(!kLagOn || kSlots >= 4, "a lagged ring needs 4 slots");
 #ifndef NERF_FP8_PF
 #define NERF_FP8_PF 1   // 1: 224 VGPRs, -1.0 % against 2 (256 VGPRs); 3 spills
 #endif
