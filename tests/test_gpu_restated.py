@@ -282,3 +282,53 @@ def test_low_gain_network_matches_restatement(tame, golden, precision):
             assert np.mean(e <= 1e-6) >= 0.999 and e.max() < 1e-3
         else:
             assert np.mean(e <= 1e-5) >= 0.998 and e.max() < 0.1
+
+
+# ------------------------------------------- fp8 saturation (the clamp branch) --
+@pytest.fixture(scope="module")
+def hot(tmp_path_factory):
+    """The low-gain networks with layer 2 amplified 10^4 x: a quarter of its outputs
+    (and some of layer 3's) run past e4m3's largest finite value (448), so the fp8
+    kernel's v_med3_f32 clamp decides what the next layers see
+    (cdna_hip_programming.md §5.4 rule 26: a rare data-dependent branch needs its
+    own test)."""
+    c = W.synthetic_state_dict(10, conditioned=False)
+    f = W.synthetic_state_dict(11, conditioned=False)
+    for sd in (c, f):
+        sd["layers.2.weight"] = sd["layers.2.weight"] * np.float32(10000.0)
+        sd["density_head.bias"] = np.full_like(sd["density_head.bias"], 2.0)    # sigma mostly > 0
+    p = tmp_path_factory.mktemp("hot") / "hot.pth"
+    W.save_checkpoint(str(p), c, f)
+    return str(p), c, f
+
+
+def test_fp8_saturation_matches_restatement(hot, golden):
+    """Activations above 448 saturate (the restatement clips them) instead of becoming
+    e4m3 NaN: every output finite, and the samples agree with the restatement as on
+    the low-gain network."""
+    from oracle import nerf_oracle as O
+
+    path, c, f = hot
+    r = _renderer(path, "fp8")
+    g = golden("mlp")
+    rng = np.random.default_rng(7)
+    pos = np.concatenate([g["pos"], rng.uniform(-6, 6, (2048, 3)).astype(np.float32)])
+    dirs = np.concatenate([g["dirs"], rng.uniform(-1.2, 1.2, (2048, 3)).astype(np.float32)])
+    pe, dpe = encodings("fp8", pos, dirs)
+    # fraction of layer-2 outputs past 448 (float64 forward of the first three layers)
+    h = pe
+    for i in range(3):
+        h = np.maximum(f[f"layers.{i}.weight"].astype(np.float64) @ h + f[f"layers.{i}.bias"][:, None], 0)
+    over = float(np.mean(h > 448.0))
+    print(f"layer-2 outputs above 448: {over:.3f}")
+    assert over > 0.1
+    for use_fine, sd, tag in ((True, f, "fine"), (False, c, "coarse")):
+        s_ref, rgb_ref = O.fp8_mlp_restated(sd, pe, dpe)
+        s, col = r.query_nerf_networks(torch.from_numpy(pos), torch.from_numpy(dirs), use_fine=use_fine)
+        s, col = s.cpu().numpy()[:, 0], col.cpu().numpy()
+        assert np.isfinite(s).all() and np.isfinite(col).all()
+        es, ec = sample_errors(s, col, s_ref, rgb_ref.T)
+        report(f"fp8 saturating net {tag} vs restatement", es, ec)
+        e = np.maximum(es, ec)
+        print(f"  samples <= 1e-5: {np.mean(e <= 1e-5):.4f}, <= 1e-4: {np.mean(e <= 1e-4):.4f}")
+        assert np.mean(e <= 1e-5) >= 0.99

@@ -287,6 +287,16 @@ def test_f32_to_e4m3_matches_torch():
     assert np.array_equal(ours, ref)
 
 
+def test_fp8_activation_round_saturates():
+    """The fp8 activation contract (mlp_fp8.hip convert_tile, oracle.fp8_activation_round):
+    ReLU and a clamp at 448 (v_med3_f32), then e4m3 RNE at scale 1 -- never NaN."""
+    x = np.array([-3.0, -0.0, 0.0, 2.0 ** -10, 3 * 2.0 ** -10, 0.3, 1.0625, 447.9, 448.0, 464.0, 1e4, 3e38],
+                 np.float32)
+    got = O.fp8_activation_round(x)
+    assert np.isfinite(got).all()
+    assert np.array_equal(got, [0.0, 0.0, 0.0, 0.0, 2.0 ** -8, 0.3125, 1.0, 448.0, 448.0, 448.0, 448.0, 448.0])
+
+
 def emulate_fp8(blob, prm, pe, dpe):
     """Kernel lane maps of the fp8 path (nerf_layout.h), float64 accumulation."""
     n = pe.shape[1]
