@@ -403,6 +403,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     Ctx cx = cx0;
     asm volatile("" : "+s"(cx.blob));   // keep the 132 chunk addresses out of SGPRs across tiles
     TrainSink sk{tro, p0, p0 < n_points, {0u, 0u}};
+#ifdef NERF_X3_ABLATE_PE_ONCE   // timing-only lab build (wrong results): encodings of the first tile reused
+    if (tile == blockIdx.x)
+#endif
     {
       float x[3], d[3], pef[32], def[16];
       const long pc = p0 < n_points ? p0 : n_points - 1;
