@@ -178,7 +178,10 @@ __device__ __forceinline__ void stage_piece(const char* __restrict__ blob, int g
   if (g >= kSlots) return;
 #endif
   char* dst = lds + (g % kSlots) * kChunkB + wave_u * 1024;
-  lds_dma_16_s(blob + size_t(g) * kChunkB, unsigned(wave_u * 1024 + lane * 16 + i * kThreads * 16),
+  // the piece's offset rides in the scalar base, so every piece shares one address
+  // VGPR (four per-piece VGPRs were spilled to AGPRs and reloaded before each piece:
+  // 3 spills and ~370 v_accvgpr_read per tile; time-neutral, bit-identical)
+  lds_dma_16_s(blob + size_t(g) * kChunkB + i * kThreads * 16, unsigned(wave_u * 1024 + lane * 16),
                lds_addr(dst + i * kThreads * 16));
 }
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
