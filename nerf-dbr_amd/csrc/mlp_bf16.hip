@@ -147,7 +147,29 @@ struct Ctx {
   // direction encodings, and of this lane half's bias rows (asm reads add an
   // immediate offset)
   unsigned ring_addr, pe_addr, de_addr, bias_addr;
+  u32x4* stg;            // NERF_BF16_REGSTAGE: this wave's pieces of the chunk in flight (VGPRs)
+  unsigned stg_addr;     // NERF_BF16_REGSTAGE: LDS address of this lane's 16 B in slot 0, piece 0
 };
+
+// NERF_BF16_REGSTAGE: chunk g's pieces -> this wave's staging VGPRs (vmcnt), and from
+// them into ring slot g % kSlots (lgkmcnt).  The asm outputs count as written at
+// issue; the seams wait vmcnt before the writes read them.
+__device__ __forceinline__ void load_chunk_regs(const Ctx& cx, int g) {
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i) {
+    const unsigned long long sb = (unsigned long long)(cx.blob + size_t(g) * kChunkB + i * kThreads * 16);
+    const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(sb)), hi = __builtin_amdgcn_readfirstlane(unsigned(sb >> 32));
+    const unsigned long long s64 = (unsigned long long)lo | ((unsigned long long)hi << 32);
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(cx.stg[i]) : "v"(unsigned(cx.wave_u * 1024 + cx.lane * 16)),
+                 "s"(s64) : "memory");
+  }
+}
+__device__ __forceinline__ void write_chunk_regs(const Ctx& cx, int g) {
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i)
+    asm volatile("ds_write_b128 %0, %1 offset:%2" :: "v"(cx.stg_addr), "v"(cx.stg[i]),
+                 "i"((g % kSlots) * kChunkB + i * kThreads * 16) : "memory");
+}
 
 // ---- LDS fragment reads from inline asm with counted waits.  Left to itself
 // hipcc puts an s_waitcnt in front of almost every MFMA (one per fragment);
@@ -165,6 +187,21 @@ NL_HD bool unit_opens_quarter(int n) {
   const int l = unit_layer(n);
   return (n - bf16_unit_base(l)) % ksteps_bf16(l) == 0;
 }
+// NERF_BF16_REGSTAGE (lab knob): the weight stream is staged through registers instead
+// of LDS-DMA -- each wave loads its pieces of a chunk into VGPRs at one seam
+// (global_load_dwordx4) and writes them to the ring at the next (ds_write_b128), so
+// those ds_writes join the LDS counts.
+#ifndef NERF_BF16_REGSTAGE
+#define NERF_BF16_REGSTAGE 0
+#endif
+NL_HD bool is_seam(int n) { return (n + kPf) % kChunkUnits == 0 && n + kPf < kUnits && n + kPf != 0; }
+NL_HD int seam_writes(int m) { return NERF_BF16_REGSTAGE && m >= 0 && m < kUnits && is_seam(m) ? kGldsPerStage : 0; }
+// writes of the seams in bodies n-kPf+1 .. n: younger than unit n's reads (issued in body n-kPf)
+NL_HD int seam_writes_since(int n) {
+  int c = 0;
+  for (int m = n - kPf + 1; m <= n; ++m) c += seam_writes(m);
+  return c;
+}
 constexpr int kBiasReads = 8 * kCols;   // 2 tiles x 4 x 16 B, per column
 NL_HD int bias_reads(int m) { return m >= 0 && m < kUnits && unit_opens_quarter(m) ? kBiasReads : 0; }
 // LDS reads younger than everything unit n consumes, at its wait
@@ -173,7 +210,7 @@ NL_HD int lgkm_for_unit(int n) {
   int c = 0;
   for (int k = n + 1; k <= n + kPf; ++k) c += unit_reads(k);
   for (int m = n - kPf + 1; m <= n; ++m) c += bias_reads(m);
-  return c;
+  return c + seam_writes_since(n);
 }
 
 // Reads of unit n into ring entry n % kRing: two A fragments (output tiles of
@@ -204,9 +241,19 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, bf16x8 (&ra)[kRi
 // The top of a tile is seam E_-1 (tile_top).
 constexpr int kDmaOutstandingAtSeam = kSlots - 3;
 constexpr int kStageAhead = kSlots - 1;   // seam g stages chunk g + kStageAhead
+static_assert(!NERF_BF16_REGSTAGE || kSlots == 3, "register staging: chunk g+2 written at seam g into chunk g-1's slot");
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
-  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
+  if (!is_seam(n)) return;
   const int g = (n + kPf) / kChunkUnits - 1;
+  if (NERF_BF16_REGSTAGE) {   // chunk g+2 (loaded at seam g-1) -> the slot chunk g-1 frees; load chunk g+3
+    wait_vmcnt(0);
+    compiler_fence();
+    __builtin_amdgcn_s_barrier();
+    compiler_fence();
+    write_chunk_regs(cx, (g + kStageAhead) % kTotalChunks);
+    load_chunk_regs(cx, (g + kStageAhead + 1) % kTotalChunks);
+    return;
+  }
   wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
   __builtin_amdgcn_s_barrier();
@@ -326,16 +373,24 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  u32x4 stg[kGldsPerStage];
   const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16,
                lds_base + kLdsPeOff + wave_u * kCols * 4096 + lane * 16,
                lds_base + kLdsDeOff + wave_u * kCols * 2048 + lane * 16,
-               lds_base + kLdsParamOff + h * 64};
+               lds_base + kLdsParamOff + h * 64, stg, lds_base + wave_u * 1024 + lane * 16};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
   // Start the weight stream (chunks 0 .. kSlots-3; each tile's top stages one
   // more) and copy the parameters, once per workgroup.
+  if (NERF_BF16_REGSTAGE) {   // chunk 0 written now, chunk 1 loaded (written at the tile top)
+    load_chunk_regs(cx0, 0);
+    wait_vmcnt(0);
+    write_chunk_regs(cx0, 0);
+    load_chunk_regs(cx0, 1);
+  } else {
 #pragma unroll
-  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+    for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+  }
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   const float* prm = (const float*)(lds + kLdsParamOff);
@@ -382,7 +437,12 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
     // previous chunk every wave finished with the last tile.
     wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
-    stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
+    if (NERF_BF16_REGSTAGE) {
+      write_chunk_regs(cx, kStageAhead - 1);
+      load_chunk_regs(cx, kStageAhead);
+    } else {
+      stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
+    }
     store_results(res, wl, res_p0, n_points, lane, out, seg, wloc);
     bf16x8 ra[kRing][2], rb[kRing][kCols];
     f32x16 acc[kCols][8];
@@ -422,7 +482,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_bf16_kernel(const char* __res
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
       // head units read two fragments each and no bias: the younger reads are
       // those of the next min(kPf, units left) units (spelled out so it folds)
-      wait_lgkm(2 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
+      wait_lgkm(2 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf) + seam_writes_since(n));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {

@@ -124,6 +124,22 @@ struct OpF16 {
   }
 };
 
+NL_HD bool is_seam(int n) { return (n + kPf) % kChunkUnits == 0 && n + kPf < kUnits && n + kPf != 0; }
+// NERF_X3_REGSTAGE (lab knob): the weight stream is staged through registers instead of
+// LDS-DMA -- each wave loads its pieces of a chunk into AGPRs at one seam
+// (global_load_dwordx4) and writes them to the ring at the next (ds_write_b128), so the
+// ds_writes join the LDS counts below.
+#ifndef NERF_X3_REGSTAGE
+#define NERF_X3_REGSTAGE 0
+#endif
+NL_HD int seam_writes(int m) { return NERF_X3_REGSTAGE && m >= 0 && m < kUnits && is_seam(m) ? kGldsPerStage : 0; }
+// writes of the seams in bodies n-kPf+1 .. n: younger than unit n's reads (issued in body n-kPf)
+NL_HD int seam_writes_since(int n) {
+  int c = 0;
+  for (int m = n - kPf + 1; m <= n; ++m) c += seam_writes(m);
+  return c;
+}
+
 // ---- compile-time unit map, as a constexpr table (this kernel is large
 // enough that the optimiser stops folding mlp_bf16.hip's loop-based map) ----
 struct UnitInfo {
@@ -157,7 +173,8 @@ constexpr UnitTable make_unit_table() {
       c = n + kPf < kUnits ? t.u[n + kPf].reads : 0;
     } else {
       for (int k = n + 1; k <= n + kPf; ++k) c += k < kUnits ? t.u[k].reads : 0;
-      for (int m = n - kPf + 1; m <= n; ++m) c += m >= 0 && t.u[m].opens ? kBiasReads : 0;
+      for (int m = n - kPf + 1; m <= n; ++m) c += (m >= 0 && t.u[m].opens ? kBiasReads : 0);
+      c += seam_writes_since(n);
     }
     t.u[n].lgkm = c;
   }
@@ -170,6 +187,8 @@ struct Ctx {
   char* lds;
   int wave_u, lane, h;
   unsigned ring_addr, pe_addr, de_addr, bias_addr, ring_hi_addr;
+  u32x4* stg;            // NERF_X3_REGSTAGE: this wave's pieces of the chunk in flight (AGPRs)
+  unsigned stg_addr;     // NERF_X3_REGSTAGE: LDS address of this lane's 16 B in slot 0, piece 0
 };
 
 __device__ __forceinline__ void stage_piece(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane,
@@ -187,6 +206,26 @@ __device__ __forceinline__ void stage_piece(const char* __restrict__ blob, int g
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g, char* lds, int wave_u, int lane) {
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i) stage_piece(blob, g, lds, wave_u, lane, i);
+}
+
+// NERF_X3_REGSTAGE: chunk g's pieces -> this wave's staging AGPRs (vmcnt), and from
+// them into ring slot g % kSlots (lgkmcnt).  The asm outputs count as written at
+// issue; the seams wait vmcnt before the writes read them.
+__device__ __forceinline__ void load_chunk_regs(const Ctx& cx, int g) {
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i) {
+    const unsigned long long sb = (unsigned long long)(cx.blob + size_t(g) * kChunkB + i * kThreads * 16);
+    const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(sb)), hi = __builtin_amdgcn_readfirstlane(unsigned(sb >> 32));
+    const unsigned long long s64 = (unsigned long long)lo | ((unsigned long long)hi << 32);
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=a"(cx.stg[i]) : "v"(unsigned(cx.wave_u * 1024 + cx.lane * 16)),
+                 "s"(s64) : "memory");
+  }
+}
+__device__ __forceinline__ void write_chunk_regs(const Ctx& cx, int g) {
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i)
+    asm volatile("ds_write_b128 %0, %1 offset:%2" :: "v"(cx.stg_addr), "a"(cx.stg[i]),
+                 "i"((g % kSlots) * kChunkB + i * kThreads * 16) : "memory");
 }
 
 template <class Op>
@@ -229,9 +268,10 @@ constexpr int kStageAhead = kSlots - 1;
 #ifndef NERF_X3_SPREAD
 #define NERF_X3_SPREAD 0
 #endif
+static_assert(!NERF_X3_SPREAD || !NERF_X3_REGSTAGE, "one staging form");
+static_assert(!NERF_X3_REGSTAGE || kSlots == 3, "register staging: chunk g+2 written at seam g into chunk g-1's slot");
 static_assert(!NERF_X3_SPREAD || (kGldsPerStage <= kChunkUnits && kSlots >= 4),
               "spread pieces land within a chunk, and need one chunk of slack at the next seam");
-NL_HD bool is_seam(int n) { return (n + kPf) % kChunkUnits == 0 && n + kPf < kUnits && n + kPf != 0; }
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if (NERF_X3_SPREAD) {
 #pragma unroll
@@ -242,6 +282,15 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   }
   if (!is_seam(n)) return;
   const int g = (n + kPf) / kChunkUnits - 1;
+  if (NERF_X3_REGSTAGE) {   // chunk g+2 (loaded at seam g-1) -> the slot chunk g-1 frees; load chunk g+3
+    wait_vmcnt(0);
+    compiler_fence();
+    __builtin_amdgcn_s_barrier();
+    compiler_fence();
+    write_chunk_regs(cx, (g + kStageAhead) % kTotalChunks);
+    load_chunk_regs(cx, (g + kStageAhead + 1) % kTotalChunks);
+    return;
+  }
   wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
 #ifndef NERF_X3_ABLATE_NOBARRIER   // timing-only lab build (wrong results): no seam barriers
@@ -374,15 +423,23 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const unsigned lds_base = lds_addr(lds);
+  u32x4 stg[kGldsPerStage];
   const Ctx cx0{blob, lds, wave_u, lane, h, lds_base + lane * 16, lds_base + kLdsPeOff + wave_u * kPeWaveB + lane * 16,
                 lds_base + kLdsDeOff + wave_u * kDeWaveB + lane * 16, lds_base + kLdsParamOff + h * 64,
-                lds_base + kLoSlots * kChunkB + lane * 16};
+                lds_base + kLoSlots * kChunkB + lane * 16, stg, lds_base + wave_u * 1024 + lane * 16};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const bool fused = !kExplicit && !kTrain && seg != nullptr;
   char* seg_slot = lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane & 31)) * 8;
 
+  if (NERF_X3_REGSTAGE) {   // chunk 0 written now, chunk 1 loaded (written at the tile top)
+    load_chunk_regs(cx0, 0);
+    wait_vmcnt(0);
+    write_chunk_regs(cx0, 0);
+    load_chunk_regs(cx0, 1);
+  } else {
 #pragma unroll
-  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+    for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, lds, wave_u, lane);
+  }
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   const float* prm = (const float*)(lds + kLdsParamOff);
@@ -440,7 +497,12 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     }
     wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
-    stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
+    if (NERF_X3_REGSTAGE) {
+      write_chunk_regs(cx, kStageAhead - 1);
+      load_chunk_regs(cx, kStageAhead);
+    } else {
+      stage_chunk(cx.blob, kStageAhead - 1, lds, wave_u, lane);
+    }
     store();
     F ra[kRing][4], rb[kRing][2];
     f32x16 acc[8];
@@ -473,7 +535,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
       const int n = kHeadUnitBase + i;
       seam_before(cx, n);
       if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
-      wait_lgkm(4 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf));
+      wait_lgkm(4 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf) + seam_writes_since(n));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
