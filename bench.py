@@ -3,8 +3,9 @@
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it
 is launched by torch.distributed.run, one process per GPU (RCCL).  A step is one
 ``render_image`` of the full 800x600 frame at 128 uniform samples per ray on the
-fine network (the reference benchmark's semantics, ``benchmark_suite.py:151-235``;
-rays/s = W*H / time, ``:216-220``).  With N GPUs each rank renders its row band
+fine network for each of the suite's two views (``generate_test_poses(2)``; the
+reference benchmark's semantics, ``benchmark_suite.py:151-235``; rays/s = W*H / the
+mean view time, ``:188-220``).  With N GPUs each rank renders its row band
 into a packed [rows, W, 4] tile (``nerf_render_band``) and the tiles are gathered
 to rank 0 over RCCL (strong scaling: the frame is fixed).
 
@@ -69,10 +70,13 @@ def sync_barrier(world):
     torch.cuda.synchronize()
 
 
-def frame_step(r, pose, width, height, spp, rank, world):
-    """One frame of renderer r as the benchmark runs it: the whole frame at N = 1
-    (render_rows, the plugin's render_image path), else this rank's band rendered
-    into the packed tile and gathered to rank 0.  Returns (step, rays in this band)."""
+def frame_step(r, poses, width, height, spp, rank, world):
+    """One step of renderer r as the benchmark runs it: one frame per pose of ``poses``
+    (the suite's protocol, benchmark_suite.py:188-220: both views of
+    generate_test_poses(2), rays/s = W*H / the mean view time), each the whole frame at
+    N = 1 (render_rows, the plugin's render_image path), else this rank's band rendered
+    into the packed tile and gathered to rank 0.  Returns (step, rays in this band per
+    frame); a step is len(poses) frames."""
     import torch
 
     from nerf_amd import distributed as D
@@ -81,14 +85,30 @@ def frame_step(r, pose, width, height, spp, rank, world):
     if world == 1:
         rgb = torch.empty(height, width, 3, device="cuda")
         dep = torch.empty(height, width, device="cuda")
-        return (lambda: r.render_rows(pose, (width, height), spp, 0, height, rgb, dep)), width * height
+
+        def step():
+            for pose in poses:
+                r.render_rows(pose, (width, height), spp, 0, height, rgb, dep)
+
+        return step, width * height
     tile = D.band_tile(world, height, width, r.torch_device())
 
     def step():
-        r.render_band(pose, (width, height), spp, r0, r1, tile)
-        D.gather_tiles_to_root(tile, width, height)
+        for pose in poses:
+            r.render_band(pose, (width, height), spp, r0, r1, tile)
+            D.gather_tiles_to_root(tile, width, height)
 
     return step, (r1 - r0) * width
+
+
+def per_view_ms(r, n_views, n_frames, stage="fine_mlp"):
+    """Mean HIP-event time of a stage per view over the last n_frames frames, which
+    alternate over the views in order."""
+    import numpy as np
+
+    hist = r.hip.stage_ms_history(min(n_frames, 64))
+    off = (-len(hist)) % n_views            # align the history's first frame with view 0
+    return [float(np.mean([f[stage] for f in hist[v + off::n_views]])) for v in range(n_views)]
 
 
 def check_gathered(r, pose, width, height, spp, rank, world):
@@ -234,10 +254,11 @@ def kernel_ms(r, n, stage="fine_mlp"):
 
 
 # ------------------------------------------------------------ README grid --
-def readme_grid(renderers, pose, rank, world):
+def readme_grid(renderers, poses, rank, world):
     """rays/s on {200x150, 400x300, 800x600} x {32, 64, 128} spp for each precision,
-    with the fractions of the MFMA roofline: ``frac_frame`` = whole-job FLOP rate /
-    (N x peak), ``frac_kernel`` = the slowest rank's fine-MLP kernel rate / peak."""
+    on the suite's two views (rays/s = W*H / mean view time), with the fractions of the
+    MFMA roofline: ``frac_frame`` = whole-job FLOP rate / (N x peak), ``frac_kernel`` =
+    the slowest rank's fine-MLP kernel rate / peak."""
     from nerf_amd import distributed as D
     from nerf_amd import weights as W
 
@@ -247,10 +268,10 @@ def readme_grid(renderers, pose, rank, world):
         rows = {}
         for (w, h) in GRID_RES:
             for spp in GRID_SPP:
-                step, band_rays = frame_step(r, pose, w, h, spp, rank, world)
-                n = 2 if prec in ("fp32", "bf16x3", "f16x3") and w * h * spp >= 400 * 300 * 128 else 4
-                dt = time_steps(step, 1, n, world)
-                kms = D.reduce_max(kernel_ms(r, n))
+                step, band_rays = frame_step(r, poses, w, h, spp, rank, world)
+                n = 1 if prec in ("fp32", "bf16x3", "f16x3") and w * h * spp >= 400 * 300 * 128 else 2
+                dt = time_steps(step, 1, n, world) / len(poses)
+                kms = D.reduce_max(kernel_ms(r, n * len(poses)))
                 flop = w * h * spp * W.FLOPS_PER_SAMPLE
                 rows[f"{w}x{h}x{spp}"] = {
                     "rays_per_s": w * h / dt, "ms_per_frame": 1e3 * dt,
@@ -273,53 +294,58 @@ def band_nan(r, pose, rows=(292, 308)):
     return rgb, dep
 
 
-def other_configs(ckpt, pose, local, ref32):
-    """The BASELINE configs besides the headline, 1 GPU each:
-    C2 400x300x64 fp32 (the parity path), C3 800x600 64+128 hierarchical bf16,
-    C5 800x600x128 fp8."""
+def other_configs(ckpt, poses, local, ref32):
+    """The BASELINE configs besides the headline, 1 GPU each, each on the
+    suite's two views (rays/s = W*H / mean view time): C2 400x300x64 fp32 (the parity
+    path), C3 800x600 64+128 hierarchical bf16, C5 800x600x128 fp8."""
     from nerf_amd import weights as W
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
 
+    nv = len(poses)
+    pose = poses[0]                  # the error bands are on view 0
     out = {}
-    step, _ = frame_step(ref32, pose, 400, 300, 64, 0, 1)
-    dt = time_steps(step, 1, 3, 1)
+    step, _ = frame_step(ref32, poses, 400, 300, 64, 0, 1)
+    dt = time_steps(step, 1, 2, 1) / nv
     out["c2_fp32_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt}
     # C2 and the headline frame on the split-fp16 path, the parity-grade fast path held to
     # the same 1e-4 gate as fp32 on the Lego fixtures (tests/test_gpu_lego.py)
     x3 = MI355XRenderer("f16x3", device_index=local)
     x3.setup(ckpt)
     x3.hip.set_profiling(True)
-    step, _ = frame_step(x3, pose, 400, 300, 64, 0, 1)
-    dt = time_steps(step, 1, 3, 1)
+    step, _ = frame_step(x3, poses, 400, 300, 64, 0, 1)
+    dt = time_steps(step, 1, 2, 1) / nv
     out["c2_f16x3_400x300x64"] = {"rays_per_s": 400 * 300 / dt, "ms_per_frame": 1e3 * dt}
-    step, _ = frame_step(x3, pose, 800, 600, 128, 0, 1)
-    dt = time_steps(step, 1, 4, 1)
-    ms = kernel_ms(x3, 4)
+    step, _ = frame_step(x3, poses, 800, 600, 128, 0, 1)
+    dt = time_steps(step, 1, 2, 1) / nv
+    ms = kernel_ms(x3, 2 * nv)
+    views_ms = per_view_ms(x3, nv, 2 * nv)
     rgb3, d3 = band_nan(x3, pose)
     rgb32, d32 = band_nan(ref32, pose)
     flop = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE
     out["gate_path_f16x3_800x600x128"] = {
         "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms,
+        "mlp_kernel_ms_per_view": views_ms,
         "mlp_tflops": flop / (ms * 1e-3) / 1e12,
         "frac_of_bf16_dense_peak": flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
         "frac_of_x3_ceiling": flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"],
         "rgb_max_abs_vs_fp32_band": float((rgb3 - rgb32).abs().max()),
         "depth_max_abs_vs_fp32_band": float((d3 - d32).abs().max()),
         "note": "the north star's two clauses side by side: this path meets the 1e-4 gate against the "
-                "reference on Lego (tests/test_gpu_lego.py) at three f16 MFMAs per product; the headline "
-                "bf16 line meets the roofline clause, not the gate"}
+                "reference on Lego (tests/test_gpu_lego.py, whole 800x600x128 frames) at three f16 MFMAs "
+                "per product; the headline bf16 line meets the roofline clause, not the gate"}
 
     h = MI355XRenderer("bf16", n_importance=128, device_index=local)
     h.setup(ckpt)
     h.hip.set_profiling(True)
-    step, _ = frame_step(h, pose, 800, 600, 64, 0, 1)
-    dt = time_steps(step, 2, 5, 1)
+    step, _ = frame_step(h, poses, 800, 600, 64, 0, 1)
+    dt = time_steps(step, 1, 3, 1) / nv
     st = h.hip.stage_ms()
     flop = 800 * 600 * (64 + 192) * W.FLOPS_PER_SAMPLE
     mlp_ms = st["coarse_mlp"] + st["fine_mlp"]
     out["c3_hierarchical_bf16_800x600_64+128"] = {
-        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms": st,
-        "mlp_tflops": flop / (mlp_ms * 1e-3) / 1e12, "mlp_frac_bf16_peak": flop / (mlp_ms * 1e-3) / 1e12 / 2500.0,
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms_last_view": st,
+        "mlp_tflops_last_view": flop / (mlp_ms * 1e-3) / 1e12,
+        "mlp_frac_bf16_peak_last_view": flop / (mlp_ms * 1e-3) / 1e12 / 2500.0,
         "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)"}
 
     # C3 on the gate-passing path (split fp16 for both nets; the hierarchical chain is
@@ -327,26 +353,28 @@ def other_configs(ckpt, pose, local, ref32):
     h3 = MI355XRenderer("f16x3", n_importance=128, device_index=local)
     h3.setup(ckpt)
     h3.hip.set_profiling(True)
-    step, _ = frame_step(h3, pose, 800, 600, 64, 0, 1)
-    dt = time_steps(step, 1, 2, 1)
+    step, _ = frame_step(h3, poses, 800, 600, 64, 0, 1)
+    dt = time_steps(step, 1, 1, 1) / nv
     st = h3.hip.stage_ms()
     mlp_ms = st["coarse_mlp"] + st["fine_mlp"]
     out["c3_hierarchical_f16x3_800x600_64+128"] = {
-        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms": st,
-        "mlp_tflops": flop / (mlp_ms * 1e-3) / 1e12, "mlp_frac_x3_ceiling": flop / (mlp_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"]}
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms_last_view": st,
+        "mlp_tflops_last_view": flop / (mlp_ms * 1e-3) / 1e12,
+        "mlp_frac_x3_ceiling_last_view": flop / (mlp_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"]}
     del h3
 
     f8 = MI355XRenderer("fp8", device_index=local)
     f8.setup(ckpt)
     f8.hip.set_profiling(True)
-    step, _ = frame_step(f8, pose, 800, 600, 128, 0, 1)
-    dt = time_steps(step, 2, 5, 1)
-    ms = kernel_ms(f8, 5)
+    step, _ = frame_step(f8, poses, 800, 600, 128, 0, 1)
+    dt = time_steps(step, 1, 3, 1) / nv
+    ms = kernel_ms(f8, 3 * nv)
     tf = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE / (ms * 1e-3) / 1e12
     rgb8, d8 = band_nan(f8, pose)
     rgb32, d32 = band_nan(ref32, pose)
     out["c5_fp8_800x600x128"] = {
-        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms, "mlp_tflops": tf,
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms,
+        "mlp_kernel_ms_per_view": per_view_ms(f8, nv, 3 * nv), "mlp_tflops": tf,
         "mlp_frac_fp8_peak": tf / PEAK_TFLOPS["fp8"],
         "rgb_max_abs_vs_fp32": float((rgb8 - rgb32).abs().max()),
         "rgb_mean_abs_vs_fp32": float((rgb8 - rgb32).abs().mean()),
@@ -354,22 +382,22 @@ def other_configs(ckpt, pose, local, ref32):
     return out, f8
 
 
-def sharded_hierarchical(ckpt, pose, local, rank, world, width, height, n_warm=2, n_steps=5):
+def sharded_hierarchical(ckpt, poses, local, rank, world, width, height, n_warm=1, n_steps=3):
     """C4: 64 coarse + 128 importance samples, bf16, each rank its row band rendered
-    into the packed tile, one gather to rank 0 per frame; rays/s of the whole frame
-    over the slowest rank."""
+    into the packed tile, one gather to rank 0 per frame, the suite's two views; rays/s
+    of the whole frame (W*H / mean view time) over the slowest rank."""
     import torch.distributed as dist
 
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
 
     h = MI355XRenderer("bf16", n_importance=128, device_index=local)
     h.setup(ckpt)
-    step, _ = frame_step(h, pose, width, height, 64, rank, world)
-    dt = time_steps(step, n_warm, n_steps, world)
+    step, _ = frame_step(h, poses, width, height, 64, rank, world)
+    dt = time_steps(step, n_warm, n_steps, world) / len(poses)
     return {"rays_per_s": width * height / dt, "ms_per_frame": 1e3 * dt, "n_gpus": world,
             "samples_per_ray": "64 coarse (coarse net) + 192 fine (fine net on the sorted union)",
             "parallelism": f"row-band x{world} + {dist.get_backend()} gather to rank 0",
-            "self_check": check_gathered(h, pose, width, height, 64, rank, world)}
+            "self_check": check_gathered(h, poses[0], width, height, 64, rank, world)}
 
 
 # ---------------------------------------------------------------- training --
@@ -645,9 +673,14 @@ def main():
     r.setup(ckpt)
     r.hip.set_profiling(True)
 
-    pose = torch.eye(4)            # benchmark_suite.generate_test_poses view 0
-    pose[2, 3] = 4.0
-    step, band_rays = frame_step(r, pose, width, height, spp, rank, world)
+    # the suite's protocol (benchmark_suite.py:188-220): both views of generate_test_poses(2),
+    # rays/s = W*H / the mean view time; a step renders view 0 then view 1
+    from nerf_amd.benchmark.benchmark_suite import generate_test_poses
+
+    poses = generate_test_poses(2)
+    nv = len(poses)
+    pose = poses[0]
+    step, band_rays = frame_step(r, poses, width, height, spp, rank, world)
 
     for _ in range(args.warmup):
         step()
@@ -660,10 +693,16 @@ def main():
         sync_barrier(world)
         elapsed = D.reduce_max(time.perf_counter() - t0)   # max over ranks
     # the fine-MLP kernel's HIP-event times of the timed frames (the library's
-    # per-frame event ring, recorded on the launch stream)
-    kern_ms = kernel_ms(r, args.steps)
+    # per-frame event ring, recorded on the launch stream), over both views and per view
+    kern_ms = kernel_ms(r, args.steps * nv)
+    kern_ms_views = per_view_ms(r, nv, args.steps * nv)
     ms_step = 1000.0 * elapsed / args.steps
-    value = width * height * args.steps / elapsed
+    value = width * height * nv * args.steps / elapsed
+    # each view timed alone as well (wall clock, same step shape), outside the timed region
+    view_ms = []
+    for p in poses:
+        vstep, _ = frame_step(r, [p], width, height, spp, rank, world)
+        view_ms.append(1e3 * time_steps(vstep, 1, max(2, args.steps // 2), world))
 
     flop_launch = band_rays * spp * W.FLOPS_PER_SAMPLE
     traffic, traffic_src = None, None
@@ -681,14 +720,17 @@ def main():
     achieved = flop_launch / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
 
-    extra = {"gpu_clock_timed_region": clocks.summary()}
+    extra = {"gpu_clock_timed_region": clocks.summary(),
+             "protocol": {"views": "generate_test_poses(2) (benchmark_suite.py:132-149, 188-220)",
+                          "frames_per_step": nv, "value": "W*H / mean view time",
+                          "ms_per_view_wall": view_ms, "mlp_kernel_ms_per_view": kern_ms_views}}
     if world > 1:
         extra["dist"] = dist_record()
         extra["self_check"] = check_gathered(r, pose, width, height, spp, rank, world)
     if world > 1 and not args.no_extras:
         # BASELINE config 4: the 64+128 hierarchical frame (bf16), sharded in row
         # bands over every rank and gathered to rank 0 -- every rank takes part
-        extra["c4_hierarchical_sharded"] = sharded_hierarchical(ckpt, pose, local, rank, world, width, height)
+        extra["c4_hierarchical_sharded"] = sharded_hierarchical(ckpt, poses, local, rank, world, width, height)
         # per-frame breakdown at N GPUs: the slowest rank's MLP kernel
         # and the exchange alone (the gather of the packed tiles), 10 frames
         tile = D.band_tile(world, height, width, r.torch_device())
@@ -719,7 +761,7 @@ def main():
         extra[f"{args.precision}_vs_fp32_depth_max_abs"] = float((d_lp - d32).abs().max())
 
     if world == 1 and not args.no_extras:
-        extra["other_configs"], f8 = other_configs(ckpt, pose, local, ref)
+        extra["other_configs"], f8 = other_configs(ckpt, poses, local, ref)
     if not args.no_extras and not args.no_grid:
         # every rank takes part (bands + gather at N > 1)
         if f8 is None:
@@ -734,7 +776,7 @@ def main():
                 rs[p] = MI355XRenderer(p, device_index=local)
                 rs[p].setup(ckpt)
                 rs[p].hip.set_profiling(True)
-        extra["readme_grid"] = readme_grid(rs, pose, rank, world)
+        extra["readme_grid"] = readme_grid(rs, poses, rank, world)
 
     if not args.no_train and not (world > 1 and args.no_extras):
         extra["training"] = training_leg(local, rank, world, args.train_steps, min(10.0, args.cpu_seconds / 3))
@@ -752,13 +794,15 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
+            "ms_per_view": ms_step / nv,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": args.precision,
             "data": ("Lego: the reference's bundled original-NeRF Lego networks (data/lego_example_weights) "
                      "distilled into NeRFModel's layout (nerf_amd/checkpoints/lego_distilled.npz, held-out PSNR "
-                     f"{lego_psnr():.1f} dB vs the teacher); suite pose view 0 (benchmark_suite.py:132-149); "
+                     f"{lego_psnr():.1f} dB vs the teacher); both suite views of generate_test_poses(2) (benchmark_suite.py:132-149), "
+                     "rays/s = W*H / mean view time (:188-220); "
                      "rays generated on the device from the pose"),
             "config": {"workload": f"render_image {width}x{height}, {spp} uniform samples/ray, fine net",
                        "resolution": [width, height], "samples_per_ray": spp,

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NERF_ABI_VERSION 4
+#define NERF_ABI_VERSION 5
 
 enum nerf_status {
   NERF_OK = 0,
@@ -35,6 +35,7 @@ enum nerf_status {
   NERF_E_HIP = -2,        /* a HIP runtime call failed                      */
   NERF_E_NO_WEIGHTS = -3, /* the requested network has not been loaded      */
   NERF_E_NO_DEVICE = -4,  /* no gfx950 device at that ordinal               */
+  NERF_E_RANGE = -5,      /* NERF_F16X3: an activation left fp16's range      */
 };
 
 enum nerf_precision {
@@ -50,7 +51,11 @@ enum nerf_precision {
                       within the 1e-4 gate of the reference renderer) */
   NERF_F16X3 = 4,  /* the same split on the f16 MFMA (v_mfma_f32_32x32x16_f16):
                       11-bit halves, ~10x closer to fp32 than NERF_BF16X3 at the
-                      same MFMA count; weights must lie in fp16's range (65504) */
+                      same MFMA count; weights must lie in fp16's range (65504:
+                      checked at load, the precision is then refused), and so must
+                      every activation and encoding input (|x| < 65520): checked on the
+                      device per sample, reported by nerf_ctx_range_status as
+                      NERF_E_RANGE, never as an inf or NaN image */
 };
 
 enum nerf_net { NERF_NET_COARSE = 0, NERF_NET_FINE = 1 };
@@ -184,13 +189,21 @@ int nerf_render_band(nerf_ctx* ctx, const float* c2w, int width, int height, int
  * The copy is queued on `stream`. */
 int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, void* stream);
 
+/* NERF_F16X3's range contract (no reference counterpart: the reference computes in fp32).
+ * Synchronizes `stream`, then returns NERF_E_RANGE if any NERF_F16X3 launch on this context
+ * since the last call met an activation or encoding input of magnitude >= 65520 (fp16's
+ * overflow: the outputs of those launches are not valid), NERF_OK otherwise; clears the
+ * flag.  The Python plugin calls it after every f16x3 render_image / query. */
+int nerf_ctx_range_status(nerf_ctx* ctx, void* stream);
+
 /* Replaces: PositionalEncoding.encode (src/models/nerf.py:31-45) for the model's two
  * encodings (n_freqs 10: positions, 4: directions): x device [n][3] -> out device
  * [n][3 + 6*n_freqs] = [x, sin(2^0 pi x), cos(2^0 pi x), sin(2^1 pi x), ...] -- the values
  * the MLP kernels of `precision` compute before rounding them to the MFMA's input type.
  * NERF_FP32 / NERF_BF16X3 / NERF_F16X3: accurate sin/cos of fl(2^k*pi)*x (sincos_acc:
  * 3-part Cody-Waite reduction by pi/2 and minimax polynomials, within 2 ulp of torch's CPU
- * sin/cos, 76 % bit-exact); NERF_BF16 / NERF_FP8: one reduced sin/cos per coordinate and lane half, then
+ * sin/cos, 76 % bit-exact; precondition |x| < 8192, so that the quotient of fl(2^9*pi*x) by
+ * pi/2 is an fp32 integer -- tested to |x| = 4e3); NERF_BF16 / NERF_FP8: one reduced sin/cos per coordinate and lane half, then
  * angle doubling (nerf_device.h). */
 int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream);
 

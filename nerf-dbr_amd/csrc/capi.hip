@@ -72,6 +72,7 @@ struct nerf_ctx {
   const float* up_zbuf = nullptr;
   const float* up_wbuf = nullptr;
   hipEvent_t stage_ev = nullptr; // recorded after the last upload from host_stage
+  int* d_range = nullptr;        // device int: an NERF_F16X3 launch saw an activation outside fp16's range
   // The stream of the last render: a render on another stream first waits for the
   // previous render's end event (its uploads and its use of the shared scratch)
   hipStream_t last_stream = nullptr;
@@ -138,7 +139,7 @@ hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, 
   if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_BF16X3) return launch_mlp_bf16x3(nd.bf16x3, nd.params, src, n, out, expl, s, seg);
-  if (precision == NERF_F16X3) return launch_mlp_f16x3(nd.f16x3, nd.params, src, n, out, expl, s, seg);
+  if (precision == NERF_F16X3) return launch_mlp_f16x3(nd.f16x3, nd.params, src, n, out, expl, s, seg, ctx->d_range);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
 }
 
@@ -175,6 +176,8 @@ int nerf_ctx_create(int device, nerf_ctx** out) {
     for (auto& e : f.ev) HIP_TRY(hipEventCreate(&e));
   HIP_TRY(hipEventCreateWithFlags(&ctx->stage_ev, hipEventDisableTiming));
   HIP_TRY(hipHostMalloc((void**)&ctx->host_stage, sizeof(float) * 2048, hipHostMallocDefault));
+  HIP_TRY(hipMalloc((void**)&ctx->d_range, sizeof(int)));
+  HIP_TRY(hipMemset(ctx->d_range, 0, sizeof(int)));
   *out = ctx;
   return NERF_OK;
 }
@@ -198,6 +201,7 @@ void nerf_ctx_destroy(nerf_ctx* ctx) {
     for (auto& e : f.ev)
       if (e) (void)hipEventDestroy(e);
   if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
+  if (ctx->d_range) (void)hipFree(ctx->d_range);
   delete ctx;
 }
 
@@ -216,9 +220,13 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
   const size_t nx3 = nerf_bf16x3_blob_bytes();
   std::vector<uint16_t> x3(nx3 / 2);
   if ((rc = nerf_pack_weights_bf16x3(params, n_params, x3.data())) != NERF_OK) return rc;
-  // fp16 halves: only when every weight fits fp16's range (else NERF_F16X3 stays unavailable)
+  // fp16 halves: only when every weight fits fp16's range (else NERF_F16X3 stays unavailable,
+  // and check_net says so when it is asked for); the probe's refusal is not this call's error
   std::vector<uint16_t> h3(nx3 / 2);
+  char saved_err[sizeof(g_err)];
+  std::memcpy(saved_err, g_err, sizeof(g_err));
   const bool have_f16x3 = nerf_pack_weights_f16x3(params, n_params, h3.data()) == NERF_OK;
+  if (!have_f16x3) std::memcpy(g_err, saved_err, sizeof(g_err));
   DeviceGuard g(ctx->device);
   NetDev& nd = ctx->net[net];
   if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
@@ -391,6 +399,9 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
   if (n_samples <= 0 || n_samples > 1024 || n_importance < 0 || n_importance > 1024 ||
       (n_importance > 0 && (n_samples < 2 || n_samples > 256)))
     return set_error(NERF_E_INVALID, "nerf_render: bad sample counts %d+%d", n_samples, n_importance);
+  // any render that gets this far may overwrite the z buffer: the last fine z stays readable
+  // only if this render's importance stage completes (set again there)
+  ctx->last_zfine = nullptr;
   const long n_rays = long(row1 - row0) * width;
   if (n_rays == 0) return NERF_OK;
   const int n_fine = n_samples + n_importance;
@@ -550,6 +561,18 @@ int nerf_render_band(nerf_ctx* ctx, const float* c2w, int width, int height, int
   return render_impl(ctx, c2w, width, height, row0, row1, focal, near_, far_, t_vals, n_samples, n_importance, u,
                      nullptr, nullptr, precision, rgbd_out, rgbd_out ? rgbd_out + 3 : nullptr, OutStrides{4, 4},
                      stream);
+}
+
+int nerf_ctx_range_status(nerf_ctx* ctx, void* stream) {
+  if (!ctx) return set_error(NERF_E_INVALID, "nerf_ctx_range_status: null context");
+  DeviceGuard g(ctx->device);
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  int flag = 0;
+  HIP_TRY(hipMemcpy(&flag, ctx->d_range, sizeof(int), hipMemcpyDeviceToHost));
+  if (flag == 0) return NERF_OK;
+  HIP_TRY(hipMemset(ctx->d_range, 0, sizeof(int)));
+  return set_error(NERF_E_RANGE, "NERF_F16X3: an activation reached fp16's range (|x| >= 65520) since the last "
+                                 "check; the outputs of those launches are not valid (use NERF_FP32 or NERF_BF16X3)");
 }
 
 int nerf_ctx_last_fine_z(nerf_ctx* ctx, long n_rays, int per_ray, float* z_out, void* stream) {

@@ -7,7 +7,7 @@ namespace nerf {
 
 hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
                              bool explicit_points, hipStream_t stream, float* seg) {
-  return launch_x3<OpBf16>(blob, params, src, n_points, out, explicit_points, stream, seg);
+  return launch_x3<OpBf16>(blob, params, src, n_points, out, explicit_points, stream, seg, nullptr);
 }
 
 hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
@@ -16,7 +16,7 @@ hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const 
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   hipLaunchKernelGGL((mlp_x3_kernel<false, true, OpBf16>), dim3(unsigned(blocks)), dim3(kThreads), 0, stream,
-                     (const char*)blob, params, src, n_points, (f32x4*)nullptr, (f32x4*)nullptr, o);
+                     (const char*)blob, params, src, n_points, (f32x4*)nullptr, (f32x4*)nullptr, o, nullptr);
   return hipGetLastError();
 }
 

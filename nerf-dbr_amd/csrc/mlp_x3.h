@@ -304,6 +304,15 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
 // Conversion schedule of mlp_bf16.hip: one dword (two values) per unit.
 NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
 NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
+// fp16 range contract (NERF_F16X3): an activation at or above 65520 converts to hi = +inf and
+// lo = f16(x - inf) = -inf, so in the next layer every row of that sample's column takes
+// w_hi.inf + w_hi.(-inf) (or 0.inf) = NaN.  One row per column is checked as each layer's
+// output tile 0 is converted (pre-ReLU, so a NaN's sign does not matter), and the heads'
+// accumulators at the end of the tile; a hit sets the caller's range flag (one vector store)
+// and the host reports NERF_E_RANGE (nerf_ctx_range_status) instead of returning the image.
+template <class Op>
+__device__ __forceinline__ bool range_checked() { return __is_same(Op, OpF16); }
+
 template <class Op>
 __device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4& fhi, u32x4& flo) {
 #ifdef NERF_X3_ABLATE_NOCONV   // timing-only lab build (wrong results): accumulator bits as fragments
@@ -371,7 +380,7 @@ __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot
 template <int L, bool kTrain, class Op, class F = typename Op::frag>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
                                          u32x4 (&ol)[16], F (&ra)[kRing][4], F (&rb)[kRing][2],
-                                         const Ctx& cx, TrainSink& sk) {
+                                         const Ctx& cx, TrainSink& sk, bool& nan_seen) {
   constexpr LayerShape sh = layer_shape(L);
   constexpr int KH = sh.hidden / 16;
   constexpr int KU = ksteps_bf16(L);
@@ -402,6 +411,8 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
           sink_dword<kTrain>(sk, L > 0 ? L - 1 : 0, 6 + t, t, acc[6 + t], pr, cx.h);
         }
         if (q >= 1 && u == dword_unit_out(KU, m)) {
+          if (!kTrain && range_checked<Op>() && q == 1 && t == 0 && pr == 0)
+            nan_seen |= __builtin_isnan(acc[0][0]);
           convert_dword<Op>(acc[2 * q - 2 + t], pr, oh[2 * (2 * q - 2 + t) + (pr >> 2)], ol[2 * (2 * q - 2 + t) + (pr >> 2)]);
           sink_dword<kTrain>(sk, L, 2 * q - 2 + t, t, acc[2 * q - 2 + t], pr, cx.h);
         }
@@ -416,7 +427,8 @@ template <bool kExplicit, bool kTrain, class Op>
 __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restrict__ blob,
                                                              const float* __restrict__ prm_g, SampleSrc src,
                                                              long n_points, f32x4* __restrict__ out,
-                                                             f32x4* __restrict__ seg, X3TrainOut tro) {
+                                                             f32x4* __restrict__ seg, X3TrainOut tro,
+                                                             int* __restrict__ range_flag) {
   typedef typename Op::frag F;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const int lane = threadIdx.x & 63;
@@ -510,15 +522,16 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     for (int n = 0; n < kPf; ++n) read_unit<Op>(cx, n, ra, rb);
 
     u32x4 aH[16], aL[16], bH[16], bL[16];
-    layer_x3<L0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
-    layer_x3<L1, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<L2, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
-    layer_x3<L3, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<L4, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // skip: [x, pe] (nerf.py:109-110)
-    layer_x3<L5, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<L6, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);
-    layer_x3<L7, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk);
-    layer_x3<C0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk);   // [x, PE4(d)] (nerf.py:117-121)
+    bool nan_seen = false;
+    layer_x3<L0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L1, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L2, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L3, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L4, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);   // skip: [x, pe] (nerf.py:109-110)
+    layer_x3<L5, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L6, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L7, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<C0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);   // [x, PE4(d)] (nerf.py:117-121)
 
     // Heads (nerf.py:114, 123-129): one tile, density row 3 over L7's fragments
     // (bH/bL, C0's input, k-steps 0..15), colour rows 0-2 over C0's output
@@ -553,6 +566,12 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
           sink_dword<kTrain>(sk, C0, 2 + (m >> 3), m >> 3, acc[2 + (m >> 3)], m & 7, h);
         }
     }
+    if (!kTrain && range_checked<Op>()) {
+      // the heads' inputs (L7's and C0's outputs) and their accumulators: rows 0-3 sit in lanes 0-31
+      nan_seen |= h == 0 && !(__builtin_isfinite(hacc[0]) && __builtin_isfinite(hacc[1]) &&
+                              __builtin_isfinite(hacc[2]) && __builtin_isfinite(hacc[3]));
+      if (nan_seen && range_flag != nullptr) *range_flag = 1;
+    }
     res = f32x4{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
     if constexpr (kTrain) {
       if (sk.valid && lane < 32) {
@@ -576,7 +595,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
 // render-pass kernel, so a variant compiles in a fifth of the time.
 template <class Op>
 hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                     bool explicit_points, hipStream_t stream, float* seg) {
+                     bool explicit_points, hipStream_t stream, float* seg, int* range_flag) {
 #ifdef NERF_X3_LAB
   if (explicit_points || !__is_same(Op, OpF16)) return hipErrorNotSupported;
 #endif
@@ -588,11 +607,11 @@ hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src
 #ifndef NERF_X3_LAB
   if (explicit_points)
     hipLaunchKernelGGL((mlp_x3_kernel<true, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,
-                       n_points, (f32x4*)out, (f32x4*)nullptr, X3TrainOut{});
+                       n_points, (f32x4*)out, (f32x4*)nullptr, X3TrainOut{}, range_flag);
   else
 #endif
     hipLaunchKernelGGL((mlp_x3_kernel<false, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,
-                       n_points, (f32x4*)out, (f32x4*)seg, X3TrainOut{});
+                       n_points, (f32x4*)out, (f32x4*)seg, X3TrainOut{}, range_flag);
   return hipGetLastError();
 }
 

@@ -1,12 +1,11 @@
 // Inline-asm building blocks shared by the MFMA kernels' weight streams.
 //
-// Why asm: when hipcc sees an LDS-DMA (global_load_lds) in a function it stops
-// counting LDS waits and emits lgkmcnt(0) before every fragment use, and left to
-// itself it puts one s_waitcnt in front of nearly every MFMA.  The kernels
-// instead issue the DMA and every in-loop LDS read from asm and wait with
-// compile-time counts.  An asm destination counts as written at the statement,
-// so every counted wait is followed by a sched_barrier that keeps the
-// consumers behind it (cdna_hip_programming.md §5.7 rule 18).
+// Why asm: when hipcc sees an LDS-DMA builtin (global_load_lds) in a function it
+// stops counting LDS waits and emits lgkmcnt(0) before every fragment use.  The
+// kernels issue the DMA from asm, which the compiler's waitcnt pass does not see (an
+// asm vector-memory op only makes the compiler's own vmcnt waits stricter), and
+// read LDS either with plain loads (default, below) or from asm with compile-time
+// counted waits (NERF_ASM_LDS_READS, lab form).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -24,24 +23,54 @@ __device__ __forceinline__ unsigned lds_addr(T* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)p;
 }
 
+// LDS fragment reads.  NERF_ASM_LDS_READS=1 issues them from asm with the counted waits
+// below; that form is unsound in general: an asm output counts as written at the
+// statement, so the register allocator may copy the destination (e.g. into an AGPR it
+// prefers for the MFMA operand) before the wait that retires the read, and the copy then
+// holds the register's old contents.  tools/lint_waits.py found exactly that in a
+// split-fp16 build (a v_accvgpr_write of a fragment 2 instructions after its ds_read, the
+// MFMA 200 instructions later reading the stale copy).  The default (0) is a plain LDS
+// load the compiler sees: its waitcnt pass then counts the reads itself and a copy is
+// placed after the data, correct by construction; wait_lgkm keeps only the scheduling
+// barrier.  `make all` lints both forms (tools/lint_waits.py).
+#ifndef NERF_ASM_LDS_READS
+#define NERF_ASM_LDS_READS 0
+#endif
+template <typename V>
+__device__ __forceinline__ const __attribute__((address_space(3))) V* lds_ptr(unsigned addr, int off) {
+  return (const __attribute__((address_space(3))) V*)(uintptr_t)(addr + unsigned(off));
+}
+
 // 16-B LDS read; off must fold to a constant in [0, 65536) after unrolling
 template <typename V>
 __device__ __forceinline__ V ds_read_b128(unsigned addr, int off) {
   static_assert(sizeof(V) == 16, "16-byte fragment");
+#if NERF_ASM_LDS_READS
   V v;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
   return v;
+#else
+  return *lds_ptr<V>(addr, off);
+#endif
 }
 __device__ __forceinline__ asm_u32x2 ds_read_b64(unsigned addr, int off) {
+#if NERF_ASM_LDS_READS
   asm_u32x2 v;
   asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
   return v;
+#else
+  return *lds_ptr<asm_u32x2>(addr, off);
+#endif
 }
 
 // s_waitcnt lgkmcnt(k), k a constant after unrolling, then a scheduling barrier
 // so nothing that consumes the reads moves above it.  The field is 4 bits on
 // gfx9: k > 15 waits at 15, i.e. for more reads than needed (safe).
 __device__ __forceinline__ void wait_lgkm(int k) {
+  if (!NERF_ASM_LDS_READS) {   // the compiler counts its own LDS reads
+    __builtin_amdgcn_sched_barrier(0);
+    return;
+  }
 #define NERF_LG(N) else if (k == N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory");
   if (k <= 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   NERF_LG(1) NERF_LG(2) NERF_LG(3) NERF_LG(4) NERF_LG(5) NERF_LG(6) NERF_LG(7) NERF_LG(8) NERF_LG(9)

@@ -36,7 +36,7 @@ def main(argv=None) -> int:
     ap.add_argument("--resolutions", default="200x150,400x300,800x600")
     ap.add_argument("--spp", default="32,64,128")
     ap.add_argument("--views", type=int, default=2)
-    ap.add_argument("--precisions", default="fp32,bf16")
+    ap.add_argument("--precisions", default="fp32,f16x3,bf16")
     ap.add_argument("--hierarchical", type=int, default=0, help="also run bf16 with N importance samples")
     ap.add_argument("--output_dir", default="outputs")
     args = ap.parse_args(argv)

@@ -144,9 +144,23 @@ class MI355XRenderer(BaseUnifiedRenderer):
         return out
 
     def render_image(self, camera_pose, resolution: Tuple[int, int], samples_per_ray: int = 64):
-        """PyTorchCPURenderer.render_image semantics (pytorch_renderers.py:127-154)."""
+        """PyTorchCPURenderer.render_image semantics (pytorch_renderers.py:127-154).  On f16x3
+        the frame is checked against fp16's activation range before it is returned
+        (NerfRangeError instead of an image with inf / NaN; nerf_ctx_range_status)."""
         width, height = resolution
-        return self.render_rows(camera_pose, resolution, samples_per_ray, 0, height)
+        out = self.render_rows(camera_pose, resolution, samples_per_ray, 0, height)
+        self.check_range()
+        return out
+
+    def check_range(self) -> None:
+        """f16x3 only: synchronize and raise NerfRangeError if a launch since the last check met
+        an activation outside fp16's range.  render_rows / render_band queue work without a host
+        synchronization; a caller of those on f16x3 calls this once its frames are done."""
+        if self.precision == "f16x3":
+            import torch
+
+            with torch.cuda.device(self.device_index):
+                self.hip.range_status()
 
     # ------------------------------------------------ granular plugin methods --
     def generate_rays(self, camera_pose, width: int, height: int, focal: float = FOCAL):
@@ -187,6 +201,7 @@ class MI355XRenderer(BaseUnifiedRenderer):
         net = rt.NERF_NET_FINE if use_fine else rt.NERF_NET_COARSE
         with torch.cuda.device(self.device_index):
             self.hip.query(net, rt.PRECISIONS[self.precision], pos, dirs, out)
+        self.check_range()
         return out[:, :1], out[:, 1:]
 
     def execute_volume_rendering(self, densities, colors, z_vals, ray_directions, with_weights: bool = False):
@@ -226,6 +241,7 @@ class MI355XRenderer(BaseUnifiedRenderer):
         w = torch.empty(n, s, dtype=torch.float32, device=dev) if with_weights else None
         with torch.cuda.device(self.device_index):
             self.hip.composite(out, 4, out[:, 1:], 4, zz, s, d, n, s, rgb, depth, acc, w)
+        self.check_range()
         return (rgb, depth, acc, w) if with_weights else (rgb, depth)
 
     def importance_sample(self, z_coarse, weights, u):

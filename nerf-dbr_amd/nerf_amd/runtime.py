@@ -69,6 +69,7 @@ SIGNATURES = {
     "nerf_render_band": (_c.c_int, [_P, _FP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float,
                                     _c.c_float, _FP, _c.c_int, _c.c_int, _FP, _c.c_int, _P, _P]),
     "nerf_ctx_last_fine_z": (_c.c_int, [_P, _c.c_long, _c.c_int, _P, _P]),
+    "nerf_ctx_range_status": (_c.c_int, [_P, _P]),
     "nerf_positional_encoding": (_c.c_int, [_c.c_int, _P, _c.c_long, _c.c_int, _P, _P]),
     "nerf_bf16x3_blob_bytes": (_c.c_size_t, []),
     "nerf_pack_weights_bf16x3": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P]),
@@ -116,6 +117,10 @@ class NerfError(RuntimeError):
     pass
 
 
+class NerfRangeError(NerfError, ArithmeticError):
+    """NERF_E_RANGE: an NERF_F16X3 launch met an activation outside fp16's range."""
+
+
 def library_path() -> str:
     return os.environ.get("NERF_MI355X_LIB", LIB_PATH)
 
@@ -138,10 +143,13 @@ def load_library() -> ctypes.CDLL:
     return lib
 
 
+NERF_E_RANGE = -5
+
+
 def _check(rc: int) -> None:
     if rc != NERF_OK:
         msg = load_library().nerf_last_error().decode(errors="replace")
-        raise NerfError(f"libnerf_mi355x error {rc}: {msg}")
+        raise (NerfRangeError if rc == NERF_E_RANGE else NerfError)(f"libnerf_mi355x error {rc}: {msg}")
 
 
 def _fptr(a: np.ndarray):
@@ -339,6 +347,11 @@ class Device:
         _check(self.lib.nerf_render_band(self._ctx, _fptr(pose), width, height, row0, row1, focal, near, far,
                                          _fptr(t), t.size, n_importance, None if uu is None else _fptr(uu),
                                          precision, _ptr(rgbd_out), _stream(stream)))
+
+    def range_status(self, stream=None) -> None:
+        """Synchronize the stream; NerfRangeError if an f16x3 launch since the last call met an
+        activation outside fp16's range (nerf_ctx_range_status)."""
+        _check(self.lib.nerf_ctx_range_status(self._ctx, _stream(stream)))
 
     def last_fine_z(self, n_rays: int, per_ray: int, out, stream=None) -> None:
         """The last hierarchical render's fine-pass sample depths [n_rays, per_ray] into out."""

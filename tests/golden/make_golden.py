@@ -4,6 +4,7 @@ Run in the development container only (the reference is not on the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --lego [/root/reference]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --lego-full [/root/reference]
 
 It imports the reference's Python renderer, model and volume-render utilities
 (bypassing ``src/benchmark/__init__.py``, whose ``numba`` import is absent here
@@ -321,9 +322,48 @@ def main_lego(ref_root: str = "/root/reference") -> None:
     print(json.dumps(meta, indent=1))
 
 
+def main_lego_full(ref_root: str = "/root/reference") -> None:
+    """The whole 800x600x128 headline frame on the Lego checkpoint, rendered by the
+    reference's own ``PyTorchCPURenderer.render_image`` (pytorch_renderers.py:127-170)
+    for suite views 0 and 1 (benchmark_suite.py:132-149, the bench's two-view protocol)
+    and the off-axis pose: render_lego_800x600_s128_full.npz (about 3 min a frame on
+    8 cores)."""
+    import torch
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    PyTorchCPURenderer, _, _, _ = import_reference(ref_root)
+    coarse_sd, fine_sd = W.lego_models()
+    ckpt_path = os.path.join(tempfile.mkdtemp(prefix="nerf_golden_lego_full_"), "lego.pth")
+    W.save_checkpoint(ckpt_path, coarse_sd, fine_sd)
+    renderer = PyTorchCPURenderer()
+    renderer.setup(ckpt_path)
+    poses = suite_poses(2) + [off_axis_pose()]
+    pose_ids = [0, 1, 2]
+    out = {"poses": np.stack([poses[i].numpy() for i in pose_ids]), "pose_ids": np.array(pose_ids, dtype=np.int32),
+           "W": np.int32(800), "H": np.int32(600), "S": np.int32(128)}
+    timing = {}
+    for k, pi in enumerate(pose_ids):
+        t0 = time.time()
+        rgb, depth = renderer.render_image(poses[pi], (800, 600), 128)
+        timing[f"800x600x128_view{pi}"] = time.time() - t0
+        print(f"view {pi}: {timing[f'800x600x128_view{pi}']:.1f} s", flush=True)
+        out[f"rgb_{k}"] = rgb.numpy()
+        out[f"depth_{k}"] = depth.numpy()
+    np.savez_compressed(os.path.join(HERE, "render_lego_800x600_s128_full.npz"), **out)
+    meta_path = os.path.join(HERE, "golden_lego_meta.json")
+    with open(meta_path) as f:
+        meta = json.load(f)
+    meta.setdefault("render_seconds", {}).update(timing)
+    meta["full_frame_digest_check"] = {"fine_digest": W.state_dict_digest(fine_sd)}
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    if "--lego" in sys.argv:
+    if "--lego-full" in sys.argv:
+        main_lego_full(args[0] if args else "/root/reference")
+    elif "--lego" in sys.argv:
         main_lego(args[0] if args else "/root/reference")
     else:
         main(args[0] if args else "/root/reference")

@@ -211,3 +211,41 @@ def test_lego_f16x3_edge_shapes_vs_oracle(ckpt, res, s):
     er, ed = maxabs(rgb, ref_rgb), maxabs(depth, ref_depth)
     print(f"lego f16x3 {res}x{s}: rgb {er:.3e} depth {ed:.3e}")
     assert er < TOL_RENDER and ed < TOL_RENDER
+
+
+FULL = "render_lego_800x600_s128_full"
+
+
+@pytest.mark.parametrize("precision", GATE)
+def test_lego_headline_full_frames_vs_reference(ckpt, golden, precision):
+    """Every pixel of the whole 800x600x128 headline frame, rendered by the reference's own
+    PyTorchCPURenderer.render_image (pytorch_renderers.py:127-170) on the Lego checkpoint for
+    the suite's views 0 and 1 and the off-axis pose (make_golden.py --lego-full): RGB and
+    depth within the 1e-4 gate on all 480,000 pixels of each frame."""
+    g = golden(FULL)
+    r = renderer(ckpt, precision)
+    for k in range(len(g["pose_ids"])):
+        rgb, depth = r.render_image(torch.from_numpy(g["poses"][k]), (800, 600), 128)
+        er, ed = maxabs(rgb, g[f"rgb_{k}"]), maxabs(depth, g[f"depth_{k}"])
+        print(f"lego {precision} 800x600x128 full frame view {int(g['pose_ids'][k])}: rgb {er:.3e} depth {ed:.3e}")
+        assert er < TOL_RENDER and ed < TOL_RENDER
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8", "bf16x3"])
+def test_lego_headline_full_frames_error_report(ckpt, golden, precision):
+    """The non-gate paths on the same whole frames, against the reference: max and mean RGB
+    error and the number of pixels whose depth differs by more than 1e-2 (the single-pixel
+    depth flips a row band would miss: a last sample with sigma ~ 0 turns a rounding-level
+    sigma into alpha ~ 1 through the reference's 1e10 last distance).  Reported; the bounds
+    only catch a broken kernel."""
+    g = golden(FULL)
+    r = renderer(ckpt, precision)
+    for k in range(len(g["pose_ids"])):
+        rgb, depth = r.render_image(torch.from_numpy(g["poses"][k]), (800, 600), 128)
+        drgb = np.abs(rgb.cpu().numpy() - g[f"rgb_{k}"])
+        ddep = np.abs(depth.cpu().numpy() - g[f"depth_{k}"])
+        n_flip = int((ddep > 1e-2).sum())
+        print(f"lego {precision} 800x600x128 full frame view {int(g['pose_ids'][k])}: rgb max {drgb.max():.3e} "
+              f"mean {drgb.mean():.3e}; depth max {ddep.max():.3e}, pixels with depth error > 1e-2: {n_flip} "
+              f"of {ddep.size}")
+        assert np.isfinite(drgb).all() and drgb.mean() < 6e-2 and n_flip < ddep.size // 10

@@ -114,6 +114,26 @@ def test_encoding_fp32_matches_reference_sincos(golden):
         assert err_ulp.max() <= 2.0
 
 
+@pytest.mark.parametrize("scale", [1e2, 1e3, 4e3])
+def test_encoding_fp32_large_coordinates(scale):
+    """sincos_acc's 3-part Cody-Waite reduction on scene coordinates far outside the Lego cube:
+    the fp32 / split paths' encodings within 2 ulp of torch's sin/cos up to |x| = 4e3 (the
+    argument fl(2^9 pi x) reaches 2e7; the header's precondition is |x| < 8192, where the
+    quotient by pi/2 still fits fp32's 24-bit integers)."""
+    from oracle import nerf_oracle as O
+
+    rng = np.random.default_rng(int(scale))
+    x = rng.uniform(-scale, scale, (20000, 3)).astype(np.float32)
+    got = gpu_encoding("fp32", x, 10)
+    ref = O.positional_encoding(torch.from_numpy(x), 10).numpy()
+    ulp = np.spacing(np.maximum(np.abs(ref), np.float32(2.0 ** -126)).astype(np.float32))
+    err_ulp = np.abs(got - ref) / ulp
+    print(f"fp32 encoding |x| <= {scale:g}: max {np.abs(got - ref).max():.2e} ({err_ulp.max():.1f} ulp), "
+          f"bit-exact {np.mean(got == ref):.4f}")
+    assert np.array_equal(got[:, :3], ref[:, :3])
+    assert err_ulp.max() <= 2.0
+
+
 def test_encoding_fast_matches_restatement():
     from oracle import nerf_oracle as O
 

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.nerf_abi_version() == 4
+    assert lib.nerf_abi_version() == 5
 
 
 def test_uniform_z_bit_exact(golden):
@@ -393,3 +393,32 @@ def test_bf16x3_packing_splits_the_bf16_stream():
     recon = set(np.round((hi_w + lo_w) * 2 ** 30).astype(np.int64).tolist())
     got = set(np.round(w_rec[nz] * 2 ** 30).astype(np.int64).tolist())
     assert recon <= got | {0}
+
+
+def test_f16x3_packing_splits_and_refuses_out_of_range():
+    """nerf_pack_weights_f16x3: the same unit layout as the split-bf16 blob with fp16 halves,
+    hi = f16(w), lo = f16(w - hi), so hi + lo carries w to ~2^-22; a weight outside fp16's
+    range (65504) is refused with NERF_E_INVALID (the loader then leaves NERF_F16X3
+    unavailable for that network)."""
+    sd = W.synthetic_state_dict(2)
+    x3 = rt.pack_weights_f16x3(sd)
+    unit = 1024
+    n_units = x3.size // (2 * unit)
+    u3 = x3.reshape(n_units, 2, unit)
+    hi = u3[:, 0].view(np.float16).astype(np.float64)
+    lo = u3[:, 1].view(np.float16).astype(np.float64)
+    assert np.all(np.isfinite(hi)) and np.all(np.isfinite(lo))
+    nz = hi != 0
+    assert np.abs(lo[nz] / hi[nz]).max() <= 2.0 ** -11 + 1e-12     # below half an fp16 ulp of hi
+    # every layer weight is reproduced by hi + lo to fp16x2 precision
+    flat = np.concatenate([sd[f"layers.{i}.weight"].ravel() for i in range(8)]).astype(np.float64)
+    rec = np.sort((hi + lo)[nz].ravel())
+    idx = np.clip(np.searchsorted(rec, flat), 1, rec.size - 1)
+    near = np.minimum(np.abs(rec[idx] - flat), np.abs(rec[idx - 1] - flat))
+    assert near.max() <= 2.0 ** -22 * np.abs(flat).max()
+    # out of range: refused, and the message says why
+    bad = dict(sd)
+    bad["layers.3.weight"] = sd["layers.3.weight"].copy()
+    bad["layers.3.weight"][5, 7] = np.float32(7e4)
+    with pytest.raises(rt.NerfError, match="fp16 range"):
+        rt.pack_weights_f16x3(bad)

@@ -177,3 +177,24 @@ def test_lego_full_render_and_band(golden, lego_nets):
     rgb, depth = O.render_image(fine, g["poses"][1], (800, 600), 128, rows=(r0, r1))
     np.testing.assert_allclose(rgb.numpy(), g["rgb_1"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(depth.numpy(), g["depth_1"], rtol=0, atol=1e-5)
+
+
+def test_lego_headline_full_frames_sampled_rows(golden, lego_nets):
+    """The whole-frame 800x600x128 fixtures (make_golden.py --lego-full, the reference's own
+    render_image on views 0, 1 and the off-axis pose): the oracle reproduces rows from the
+    top, the middle and the bottom of every frame; consistent with the headline band fixture
+    where they overlap."""
+    _, fine = lego_nets
+    g = golden("render_lego_800x600_s128_full")
+    assert (int(g["W"]), int(g["H"]), int(g["S"])) == (800, 600, 128)
+    for k in range(len(g["pose_ids"])):
+        assert g[f"rgb_{k}"].shape == (600, 800, 3) and g[f"depth_{k}"].shape == (600, 800)
+        for r0 in (0, 297, 599):
+            rgb, depth = O.render_image(fine, g["poses"][k], (800, 600), 128, rows=(r0, r0 + 1))
+            np.testing.assert_allclose(rgb.numpy(), g[f"rgb_{k}"][r0:r0 + 1], rtol=0, atol=1e-5)
+            np.testing.assert_allclose(depth.numpy(), g[f"depth_{k}"][r0:r0 + 1], rtol=0, atol=1e-5)
+    band = golden("render_lego_800x600_s128_band")
+    b0, b1 = map(int, band["rows"])
+    for kb, kf in ((0, 0), (1, 2)):                    # band views: suite view 0, off-axis
+        np.testing.assert_array_equal(band[f"rgb_{kb}"], g[f"rgb_{kf}"][b0:b1])
+        np.testing.assert_array_equal(band[f"depth_{kb}"], g[f"depth_{kf}"][b0:b1])
