@@ -202,8 +202,10 @@ int nerf_ctx_range_status(nerf_ctx* ctx, void* stream);
  * the MLP kernels of `precision` compute before rounding them to the MFMA's input type.
  * NERF_FP32 / NERF_BF16X3 / NERF_F16X3: accurate sin/cos of fl(2^k*pi)*x (sincos_acc:
  * 3-part Cody-Waite reduction by pi/2 and minimax polynomials, within 2 ulp of torch's CPU
- * sin/cos, 76 % bit-exact; precondition |x| < 8192, so that the quotient of fl(2^9*pi*x) by
- * pi/2 is an fp32 integer -- tested to |x| = 4e3); NERF_BF16 / NERF_FP8: one reduced sin/cos per coordinate and lane half, then
+ * sin/cos for |x| <= 1e3 and 3 ulp at 4e3 (the reduction's second step rounds at the reduced
+ * argument's ulp), 76 % bit-exact; precondition |x| < 8192, so that the quotient of
+ * fl(2^9*pi*x) by pi/2 is an fp32 integer); NERF_BF16 / NERF_FP8: one reduced sin/cos per
+ * coordinate and lane half, then
  * angle doubling (nerf_device.h). */
 int nerf_positional_encoding(int precision, const float* x, long n, int n_freqs, float* out, void* stream);
 

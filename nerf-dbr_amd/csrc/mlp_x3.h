@@ -24,7 +24,7 @@
 //   * 4 waves x 32 samples = 128 samples per workgroup tile;
 //   * weight units of 4 KiB = the bf16 kernel's 2 KiB unit of W_hi, then W_lo
 //     (nerf_pack_weights_bf16x3 / _f16x3), 4 units per 16 KiB chunk, 3-slot ring;
-//   * encodings are the accurate fp32 ones (the fp32 path's sincosf), split
+//   * encodings are the accurate fp32 ones (sincos_acc, as the fp32 path; the training kernels keep ocml sincosf), split
 //     into hi and lo fragments in LDS;
 //   * the ReLU'd fp32 activations are split as they are converted:
 //     hi = T(relu x), lo = T(relu x - hi).

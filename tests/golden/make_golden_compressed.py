@@ -3,6 +3,7 @@
 Run in the development container only (the reference is not on the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_compressed.py [/root/reference]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_compressed.py --lego [/root/reference]
 
 Imports src/benchmark/compressed_renderer.py (default config: 10 % magnitude
 pruning and int8 asymmetric per-tensor quantisation of every weight and bias,
@@ -10,6 +11,9 @@ fp16 linear layers, fp16 compositing with a 1e4 last interval), sets it up on
 the same deterministic synthetic checkpoint as make_golden.py, and records:
   compressed.npz  query_nerf_networks (fine) on the first 512 points of mlp.npz,
                   and render_image at 32x24, 16 samples, suite view 0.
+  compressed_lego.npz (--lego)  render_image on the distilled Lego checkpoint at
+                  200x150, 32 samples, suite view 0 and the off-axis pose of make_golden.py:
+                  config 5's error baseline on the content BASELINE names.
 These pin the oracle's restatement (oracle/nerf_oracle.py, compressed_*), which
 is the error baseline the fp8 path is reported against; the reference's
 compressed renderer is not a parity target.
@@ -28,6 +32,41 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "nerf-dbr_amd"))
 
 from nerf_amd import weights as W  # noqa: E402
+
+
+def _import(ref_root):
+    sys.path.insert(0, ref_root)
+    import src  # noqa: F401
+
+    bp = types.ModuleType("src.benchmark")
+    bp.__path__ = [os.path.join(ref_root, "src", "benchmark")]
+    sys.modules["src.benchmark"] = bp
+    from src.benchmark.compressed_renderer import CompressedNeRFRenderer
+
+    return CompressedNeRFRenderer
+
+
+def main_lego(ref_root: str = "/root/reference") -> None:
+    import torch
+
+    sys.path.insert(0, HERE)
+    from make_golden import off_axis_pose, suite_poses
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    CompressedNeRFRenderer = _import(ref_root)
+    ckpt = W.write_lego_checkpoint(os.path.join(tempfile.mkdtemp(), "lego.pth"))
+    r = CompressedNeRFRenderer()
+    r.setup(ckpt)
+    poses = [suite_poses(2)[0], off_axis_pose()]
+    out = {"poses": np.stack([p.numpy() for p in poses]), "pose_ids": np.array([0, 2], dtype=np.int32),
+           "W": np.int32(200), "H": np.int32(150), "S": np.int32(32)}
+    with torch.no_grad():
+        for k, p in enumerate(poses):
+            img, depth = r.render_image(p, (200, 150), 32)
+            out[f"rgb_{k}"] = img.float().numpy()
+            out[f"depth_{k}"] = depth.float().numpy()
+    np.savez_compressed(os.path.join(HERE, "compressed_lego.npz"), **out)
+    print("compressed_lego.npz:", out["rgb_0"].shape)
 
 
 def main(ref_root: str = "/root/reference") -> None:
@@ -58,4 +97,5 @@ def main(ref_root: str = "/root/reference") -> None:
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    (main_lego if "--lego" in sys.argv else main)(args[0] if args else "/root/reference")

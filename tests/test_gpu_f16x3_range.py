@@ -57,15 +57,20 @@ def _scaled(sd, factor):
 @pytest.fixture(scope="module")
 def nets(tmp_path_factory):
     """Three versions of one low-gain network: layer 2 scaled so that the largest activation
-    lands at ~2e4 (inside fp16's range), and at ~1e6 (far outside)."""
+    lands at ~2e4 (inside fp16's range), and at ~1.5e5 (outside it; the weights still fit)."""
     base = W.synthetic_state_dict(21, conditioned=False)
     pos, _ = _points()
     m0 = _max_activation(base, pos)
     d = tmp_path_factory.mktemp("f16range")
     out = {}
-    for tag, target in (("inside", 2.0e4), ("outside", 1.0e6)):
-        sd = _scaled(base, target / m0)
-        m = _max_activation(sd, pos)
+    for tag, target in (("inside", 2.0e4), ("outside", 1.5e5)):   # layer 2's weights stay inside fp16
+        # the largest activation is not linear in the factor (layers 0-1 are unscaled, biases
+        # follow), so a few fixed-point steps land it near the target
+        f = target / m0
+        for _ in range(6):
+            sd = _scaled(base, f)
+            m = _max_activation(sd, pos)
+            f *= target / m
         p = str(d / f"{tag}.pth")
         W.save_checkpoint(p, sd, sd)
         out[tag] = (p, m)
@@ -137,8 +142,9 @@ def test_f16x3_refused_for_out_of_range_weights(tmp_path):
     pos, dirs = _points(128)
     r = _renderer(p_ok, "f16x3")
     r.query_nerf_networks(pos, dirs)
+    before = rt.load_library().nerf_last_error().decode()
     r.setup(p_big)                                   # reload over a valid net
-    assert "fp16" not in rt.load_library().nerf_last_error().decode()
+    assert rt.load_library().nerf_last_error().decode() == before   # the probe's refusal is not the load's error
     with pytest.raises(rt.NerfError, match="fp16"):
         r.query_nerf_networks(pos, dirs)
     for prec in ("fp32", "bf16", "bf16x3"):

@@ -479,7 +479,9 @@ def test_bench_single_gpu_json_contract():
         assert k in b, k
     assert b["n_gpus"] == 1 and b["steps"] == 3 and b["warmup"] == 1 and b["dtype"] == "bf16"
     assert b["higher_is_better"] is True and b["vs_baseline"] is None and "workload" in b["config"]
-    assert b["value"] == pytest.approx(160 * 120 / (b["ms_per_step"] * 1e-3), rel=1e-6)
+    # a step renders both suite views (benchmark_suite.py:188-220): value = W*H / mean view time
+    assert b["protocol"]["frames_per_step"] == 2 and b["ms_per_view"] == pytest.approx(b["ms_per_step"] / 2)
+    assert b["value"] == pytest.approx(160 * 120 / (b["ms_per_view"] * 1e-3), rel=1e-6)
     rf = b["roofline"]
     assert rf["bound"] == "mfma" and rf["unit"] == "TFLOP/s" and rf["peak"] == 2500.0
     assert 0 < rf["achieved"] and rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"])

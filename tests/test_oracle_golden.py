@@ -198,3 +198,16 @@ def test_lego_headline_full_frames_sampled_rows(golden, lego_nets):
     for kb, kf in ((0, 0), (1, 2)):                    # band views: suite view 0, off-axis
         np.testing.assert_array_equal(band[f"rgb_{kb}"], g[f"rgb_{kf}"][b0:b1])
         np.testing.assert_array_equal(band[f"depth_{kb}"], g[f"depth_{kf}"][b0:b1])
+
+
+def test_compressed_restatement_on_lego(golden):
+    """Config 5's error baseline on Lego: the oracle's restatement of the reference's int8
+    compressed renderer reproduces the reference's own render (make_golden_compressed.py
+    --lego) of the distilled checkpoint at 200x150x32, bit for bit."""
+    g = golden("compressed_lego")
+    _, f = W.lego_models()
+    cw = O.compressed_weights(f)
+    for k in range(len(g["pose_ids"])):
+        rgb, depth = O.compressed_render_image(cw, torch.from_numpy(g["poses"][k]), (200, 150), 32)
+        np.testing.assert_array_equal(rgb.numpy(), g[f"rgb_{k}"])
+        np.testing.assert_array_equal(depth.numpy(), g[f"depth_{k}"])

@@ -10,6 +10,8 @@ rc=$?
 echo "suite rc=$rc"; grep -E "^FAILED|passed|failed" $OUT/gpu_suite.log | tail -8
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $OUT/smoke.log; exit 1; }
+timeout -k 10 120 tools/probes/x3_shape_probe 24 > $OUT/x3_shape_probe.txt 2>&1 || { echo "probe rc=$?"; tail -5 $OUT/x3_shape_probe.txt; exit 1; }
+tail -6 $OUT/x3_shape_probe.txt
 for p in bf16 fp8 f16x3; do
   timeout -k 10 200 python -u tools/kernel_lab.py --precision $p --rounds 11 nerf-dbr_amd/nerf_amd/_lib/libnerf_mi355x.so labx/libnerf_asmreads.so > $OUT/lab_$p.json 2> $OUT/lab_$p.err || { echo "lab $p rc=$?"; tail -5 $OUT/lab_$p.err; exit 1; }
 done

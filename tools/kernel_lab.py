@@ -68,11 +68,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--spp", type=int, default=128)
     ap.add_argument("--ckpt", choices=["lego", "synthetic"], default="lego")
+    # the same instruction stream on different operand values: "lab" (camera on +z at 4),
+    # or view 0 / view 1 of the suite's generate_test_poses(2) (view 1 is near-empty content)
+    ap.add_argument("--pose", choices=["lab", "view0", "view1"], default="lab")
     args = ap.parse_args()
     _, fine = W.lego_models() if args.ckpt == "lego" else W.synthetic_models(0)
     libs = [Lib(p, fine, rt.PRECISIONS[args.precision]) for p in args.libs]
     pose = np.eye(4, dtype=np.float32)
     pose[2, 3] = 4.0
+    if args.pose != "lab":
+        from nerf_amd.benchmark.benchmark_suite import generate_test_poses
+
+        pose = np.ascontiguousarray(generate_test_poses(2)[int(args.pose[-1])].numpy().astype(np.float32))
     t = torch.linspace(0, 1, args.spp).numpy()
     rgb = torch.empty(600, 800, 3, device="cuda")
     depth = torch.empty(600, 800, device="cuda")

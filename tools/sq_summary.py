@@ -13,6 +13,15 @@ import os
 import sys
 
 
+def _lab_ms(path):
+    """median_ms from the kernel_lab.py JSON a counter pass printed, or None."""
+    try:
+        txt = open(path).read()
+        return float(next(iter(json.loads(txt[txt.index("{"):txt.rindex("}") + 1]).values()))["median_ms"])
+    except (OSError, ValueError, StopIteration, KeyError):
+        return None
+
+
 def main(src, dest, prec):
     cnt = {}
     for p in ("p1", "p2"):
@@ -29,7 +38,11 @@ def main(src, dest, prec):
          "lds_insts_per_mfma": cnt["SQ_INSTS_LDS"] / cnt["SQ_INSTS_MFMA"],
          "lds_bank_conflict_cycles": cnt["SQ_LDS_BANK_CONFLICT"]}
     summ = os.path.join(dest, "summary.json")
-    if os.path.exists(summ):
+    lab = _lab_ms(os.path.join(src, "p2.log"))
+    if lab:   # the counter pass's own kernel time (kernel_lab.py's HIP events, same dispatches)
+        d["kernel_ms_counter_pass"] = lab
+        d["effective_clock_ghz"] = cycles_xcd / (lab * 1e-3) / 1e9
+    elif os.path.exists(summ):
         key = {"f16x3": "mlp_x3_kernel<OpF16>", "bf16x3": "mlp_x3_kernel<OpBf16>"}.get(prec, f"mlp_{prec}_kernel")
         k = json.load(open(summ))["kernels"].get(key)
         if k:
