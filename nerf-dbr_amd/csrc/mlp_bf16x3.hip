@@ -1,6 +1,7 @@
 // NERF_BF16X3: the split-bf16 instantiations of mlp_x3.h (the render pass, explicit
-// points and the training forward).  Built without -amdgpu-mfma-vgpr-form: with it the
-// explicit-points bf16 instantiation computed wrong sigmas (round 3), the f16 ones not.
+// points and the training forward).  Built with -amdgpu-mfma-vgpr-form like the f16 unit
+// (-2.2 %, bit-identical); round 3's wrong sigmas under that flag came from the asm
+// fragment reads' waits, which the compiler now counts (nerf_asm.h, Makefile).
 #include "mlp_x3.h"
 
 namespace nerf {

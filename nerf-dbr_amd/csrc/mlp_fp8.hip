@@ -7,9 +7,10 @@
 // Same network, orientation and schedule as mlp_bf16.hip (nerf_layout.h):
 // H^T = W . X^T on 32x32 tiles, the accumulator of one layer is the B operand
 // of the next, 8 waves x 32 samples, quarter schedule, an LDS ring filled by
-// LDS-DMA with one barrier per chunk, asm fragment reads with counted waits.
+// LDS-DMA with one barrier per chunk, compiler-counted fragment reads.
 // What differs:
-//   * waves 4-7 run one chunk behind waves 0-3 (NERF_FP8_LAG below);
+//   * waves 4-7 run one chunk behind waves 0-3 (the wave lag below), and one
+//     workgroup per CU loops over the tiles with the weight stream running on;
 //   * k-steps are 64 wide: a hidden k-step takes accumulator tiles 2u, 2u+1;
 //     a 256-wide layer has 4 k-steps (vs 16 in bf16), each MFMA is 64 cycles
 //     and does 4x the work of a bf16 one, at twice the bf16 FLOP rate;
@@ -53,43 +54,44 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;           // 256
 constexpr int kUnitB = kFp8UnitBytes;                                // 4 KiB: 2 tiles x 64 lanes x 32 B
 constexpr int kUnits = kFp8Units + kFp8HeadUnits;                    // 134
-#ifndef NERF_FP8_CHUNK_UNITS
-#define NERF_FP8_CHUNK_UNITS 4       // 4 KiB units per LDS chunk (one barrier per chunk)
-#endif
-constexpr int kChunkUnits = NERF_FP8_CHUNK_UNITS;
+constexpr int kChunkUnits = 4;                                       // 4 KiB units per LDS chunk (one barrier per chunk)
 constexpr int kChunkB = kChunkUnits * kUnitB;                        // 16 KiB
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;
-#ifndef NERF_FP8_SLOTS
-#define NERF_FP8_SLOTS 4
-#endif
-constexpr int kSlots = NERF_FP8_SLOTS;
+constexpr int kSlots = 4;
 // Wave lag: waves 4-7 run one chunk behind waves 0-3, so the two waves of a
-// SIMD reach their layer boundaries (scale reduction and conversion, nothing
-// for the MFMA pipe) at different times.  The ring then holds one chunk more
-// for the lagging half: every wave stages one chunk less far ahead, and the
-// lagging half's seam g is barrier instance g + 1 (one extra barrier at its
-// start, one at the leading half's end).  Measured -1.6 % kernel time,
-// bit-identical output; a 5-slot ring (restoring the staging distance) was
-// slower (-1.1 %).  Timing ablations and other lab variants of round 1
-//  are not part of this source.
-#ifndef NERF_FP8_LAG
-#define NERF_FP8_LAG 1
-#endif
-constexpr int kLagOn = NERF_FP8_LAG;
-static_assert(!kLagOn || kSlots >= 4, "a lagged ring needs 4 slots");
+// SIMD reach their layer boundaries (the conversion of the last quarter's tiles,
+// nothing for the MFMA pipe) at different times.  The ring holds one chunk more
+// for the lagging half: every wave stages one chunk ahead of the chunk it
+// publishes, and the lagging half's seam for chunk c is barrier instance c + 1
+// (one extra barrier at its start, one at the leading half's end).  Measured
+// -1.6 % kernel time, bit-identical output.
+//
+// Persistent tiles (round 4): one workgroup per CU loops over 256-sample tiles and
+// the weight stream runs on across them -- a tile's last seams stage the next
+// tile's first chunks -- so the ring is never refilled, the parameters and row
+// scales are copied once per workgroup, and no workgroup is relaunched.  A tile is
+// kTotalChunks = 34 chunks and 34 = 2 mod 4, so the ring slot of a tile's chunk c
+// is (c + rot) mod 4 with rot = 2 * (tile iteration mod 2), which is only known at
+// run time: a fragment read of chunk c uses base ring_lo (= ring + rot slots) for
+// c mod 4 in {0, 1} and ring_hi (= ring - rot slots) for {2, 3} with the same
+// immediate offset as before (the ring sits 2 slots above the LDS base, so ring_hi
+// stays a valid address), and a stage's LDS slot is a scalar (c + rot) & 3.
+constexpr int kGldsPerStage = kChunkB / (kThreads * 16);
 #ifndef NERF_FP8_PF
-#define NERF_FP8_PF 1   // 1: 224 VGPRs, -1.0 % against 2 (256 VGPRs); 3 spills
+#define NERF_FP8_PF 1   // 1: -1.0 % against 2 (round 1)
 #endif
 constexpr int kPf = NERF_FP8_PF;                                     // fragment prefetch distance (units)
 constexpr int kRing = kPf + 1;
-constexpr int kGldsPerStage = kChunkB / (kThreads * 16);
+static_assert(kUnits % kRing == 0, "the next tile's unit n uses ring entry n % kRing, as this tile's");
+static_assert(kChunkUnits == 4 && kTotalChunks == 34 && kTotalChunks % 2 == 0 && kTotalChunks % kSlots == 2,
+              "the ring rotation assumes 34 four-unit chunks per tile in a 4-slot ring");
 static_assert(kTotalChunks * kChunkB <= kFp8ScaleOff, "ring reads stay inside the padded fragment area");
-// slots 0-3 are read at ring_addr + offset, a fifth at ring_hi_addr (ds_read offsets are 16 bits)
-constexpr int kLoSlots = 65536 / kChunkB;
-static_assert(kSlots <= kLoSlots + 1 && kLoSlots * kChunkB <= 65536, "ring offsets must fit the ds_read offset field");
-constexpr int kLdsParamOff = kSlots * kChunkB;
-constexpr int kLdsScaleOff = kLdsParamOff + ((kParamFloats * 4 + 1023) / 1024) * 1024;
-constexpr int kLdsPeOff = kLdsScaleOff + kFp8ScaleBytes;
+constexpr int kLdsParamOff = 0;
+constexpr int kLdsScaleOff = ((kParamFloats * 4 + 1023) / 1024) * 1024;
+constexpr int kLdsRingOff = kLdsScaleOff + kFp8ScaleBytes;
+static_assert(kLdsRingOff >= 2 * kChunkB, "ring_hi = ring - 2 slots must stay a valid LDS address");
+static_assert(kLdsRingOff % 16 == 0 && kSlots * kChunkB <= 65536, "ring offsets fit the ds_read offset field");
+constexpr int kLdsPeOff = kLdsRingOff + kSlots * kChunkB;
 constexpr int kLdsDeOff = kLdsPeOff + kWaves * 2048;
 constexpr int kLdsSegOff = kLdsDeOff + kWaves * 2048;                 // fused compositing: (dist, z) per sample
 constexpr int kLdsBytes = kLdsSegOff + kWaves * kSamplesPerWave * 8;
@@ -98,82 +100,88 @@ constexpr int kDeFromPe = kLdsDeOff - kLdsPeOff;                      // one add
 static_assert(kDeFromPe + 1024 + 16 <= 65536, "direction reads fit the ds_read offset field");
 static_assert(kFp8ScaleBytes % 16 == 0 && kLdsScaleOff % 16 == 0, "16-B aligned carve");
 
-// ---- compile-time unit map (units kFp8Units.. are the heads') ----
-NL_HD bool unit_is_head(int n) { return n >= kFp8Units; }
-NL_HD int unit_layer(int n) {
-  int l = 0;
-  while (l + 1 < kNumMfmaLayers && fp8_unit_base(l + 1) <= n) ++l;
-  return l;
-}
-NL_HD int unit_kstep(int n) { return (n - fp8_unit_base(unit_layer(n))) % ksteps_fp8(unit_layer(n)); }
-NL_HD int unit_extra(int n) {
-  if (unit_is_head(n)) return 0;
-  const int l = unit_layer(n);
-  return unit_kstep(n) < layer_shape(l).hidden / 64 ? 0 : layer_shape(l).extra;
-}
-NL_HD bool unit_opens_quarter(int n) { return !unit_is_head(n) && unit_kstep(n) == 0; }
-NL_HD int unit_reads(int n) { return n < 0 || n >= kUnits ? 0 : 4 + (unit_extra(n) != 0 ? 2 : 0); }
+// ---- compile-time unit map (units kFp8Units.. are the heads'), a constexpr table:
+// inside the tile loop LLVM stops constant-folding a loop-based map at this body
+// size and evaluates it at run time (as mlp_x3.h found) ----
 constexpr int kQuarterReads = 8 + 1;          // bias (2 tiles x 4 x 16 B) + the weight-scale pair
-// the reads a unit body issues before its prefetch: a quarter's bias and weight
-// scales, or the density row's scale at the first head unit
-NL_HD int quarter_reads(int m) {
-  return m >= 0 && m < kUnits && unit_opens_quarter(m) ? kQuarterReads : (m == kFp8Units ? 1 : 0);
+struct UnitInfo {
+  int layer, kstep, extra, reads, qreads, lgkm;
+  bool opens;
+};
+struct UnitTable {
+  UnitInfo u[kUnits];
+};
+constexpr UnitTable make_unit_table() {
+  UnitTable t{};
+  for (int n = 0; n < kUnits; ++n) {
+    UnitInfo& x = t.u[n];
+    if (n >= kFp8Units) {                     // heads: the density row's scale at the first
+      x = UnitInfo{-1, n - kFp8Units, 0, 4, n == kFp8Units ? 1 : 0, 0, false};
+      continue;
+    }
+    int l = 0;
+    while (l + 1 < kNumMfmaLayers && fp8_unit_base(l + 1) <= n) ++l;
+    const int ks = (n - fp8_unit_base(l)) % ksteps_fp8(l);
+    const int ex = ks < layer_shape(l).hidden / 64 ? 0 : layer_shape(l).extra;
+    x = UnitInfo{l, ks, ex, 4 + (ex != 0 ? 2 : 0), ks == 0 ? kQuarterReads : 0, 0, ks == 0};
+  }
+  // Issue order per unit body m: [qreads(m)], reads of unit m+kPf, wait, MFMAs.
+  // LDS reads younger than all unit n needs:
+  for (int n = 0; n < kUnits; ++n) {
+    int c = 0;
+    if (t.u[n].qreads > 0) {
+      c = n + kPf < kUnits ? t.u[n + kPf].reads : 0;
+    } else {
+      for (int k = n + 1; k <= n + kPf; ++k) c += k < kUnits ? t.u[k].reads : 0;
+      for (int m = n - kPf + 1; m <= n; ++m) c += m >= 0 ? t.u[m].qreads : 0;
+    }
+    t.u[n].lgkm = c;
+  }
+  return t;
 }
-// Issue order per unit body m: [quarter_reads(m)], reads of unit m+kPf, wait,
-// MFMAs.  LDS reads younger than all unit n needs:
-NL_HD int lgkm_for_unit(int n) {
-  if (quarter_reads(n) > 0) return unit_reads(n + kPf);
-  int c = 0;
-  for (int k = n + 1; k <= n + kPf; ++k) c += unit_reads(k);
-  for (int m = n - kPf + 1; m <= n; ++m) c += quarter_reads(m);
-  return c;
-}
+constexpr UnitTable kTab = make_unit_table();
+NL_HD int unit_extra(int n) { return kTab.u[n].extra; }
+NL_HD int lgkm_for_unit(int n) { return kTab.u[n].lgkm; }
 
 struct Ctx {
   const char* blob;
   char* lds;
+  unsigned lds_base;                                            // LDS byte address of lds[0]
   int wave_u, lane, h;
-  unsigned ring_addr, pe_addr, bias_addr, scale_addr;   // direction slots: pe_addr + kDeFromPe
-  unsigned ring_hi_addr;                                 // ring slot kLoSlots (5-slot ring only)
-  int lag;                                               // 1: this wave runs a chunk behind (NERF_FP8_LAG)
+  unsigned ring_lo, ring_hi, pe_addr, bias_addr, scale_addr;   // direction slots: pe_addr + kDeFromPe
+  int rot;                                                      // ring rotation of this tile (0 or 2), wave-uniform
+  int lag;                                                      // 1: this wave runs a chunk behind
 };
 
-// Stage chunk g + lag (g a constant after unrolling, lag wave-uniform 0 or 1).
-__device__ __forceinline__ void stage_chunk(const Ctx& cx, int g, int lag = 0) {
-  const int s0 = g % kSlots;
-  const int slot = s0 + lag == kSlots ? 0 : s0 + lag;
-  char* dst = cx.lds + slot * kChunkB + cx.wave_u * 1024;
+// Stage this wave's pieces of the tile's chunk c (a constant after unrolling; c >= 34
+// is the next tile's chunk c - 34, whose slot the same rotation gives).
+__device__ __forceinline__ void stage_chunk(const Ctx& cx, int c) {
+  const int slot = (c + cx.rot) & (kSlots - 1);
+  const unsigned dst = cx.lds_base + unsigned(kLdsRingOff + slot * kChunkB + cx.wave_u * 1024);
+  const int src = c < kTotalChunks ? c : c - kTotalChunks;
 #pragma unroll
   for (int i = 0; i < kGldsPerStage; ++i)
-    lds_dma_16_s(cx.blob + size_t(g + lag) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
-                 lds_addr(dst + i * kThreads * 16));
+    lds_dma_16_s(cx.blob + size_t(src) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
+                 dst + unsigned(i * kThreads * 16));
 }
 
-NL_HD int dma_outstanding_at_seam(int g) {
-  const int issued_last = (g + kSlots - 2 < kTotalChunks - 1) ? g + kSlots - 2 : kTotalChunks - 1;
-  return issued_last > g + 1 ? issued_last - (g + 1) : 0;
-}
-// Seam before the prefetch reaches chunk g+1 (protocol of mlp_bf16.hip):
-// own pieces of g+1 landed, barrier, restage chunk g-1's slot with g+kSlots-1.
-__device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
-  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits || n + kPf == 0) return;
-  const int g = (n + kPf) / kChunkUnits - 1;
-  if (kLagOn) {
-    // own pieces of chunk g+1+lag landed: stages younger than it are those of
-    // chunks up to g+lag+kSlots-3 (one fewer near the end; a smaller count only waits longer)
-    int younger = kSlots - 4 < kTotalChunks - 3 - g ? kSlots - 4 : kTotalChunks - 3 - g;
-    wait_vmcnt(kGldsPerStage * (younger > 0 ? younger : 0));
-  } else {
-    wait_vmcnt(kGldsPerStage * dma_outstanding_at_seam(g));
-  }
+// Seam before this wave's first read of the tile's chunk c: its own pieces of c
+// landed (nothing younger is in flight: vmcnt(0)), the barrier publishes c to every
+// wave and frees the slot of chunk c - 3 (the lagging half finished it a barrier
+// ago), which takes chunk c + 1 (leading half) or c + 2 (lagging half): at barrier
+// instance k both halves stage global chunk k + 1.
+__device__ __forceinline__ void seam(const Ctx& cx, int c) {
+  wait_vmcnt(0);
   compiler_fence();
   __builtin_amdgcn_s_barrier();
   compiler_fence();
-  if (kLagOn) {
-    if (g + cx.lag + kSlots - 2 < kTotalChunks) stage_chunk(cx, g + kSlots - 2, cx.lag);
-  } else if (g + kSlots - 1 < kTotalChunks) {
-    stage_chunk(cx, g + kSlots - 1);
-  }
+  stage_chunk(cx, c + 1 + cx.lag);
+}
+// The seam inside the unit sequence: before unit body n when its prefetch (unit
+// n + kPf) is the first unit of a chunk.
+__device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
+  if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits) return;
+  seam(cx, (n + kPf) / kChunkUnits);
 }
 
 __device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
@@ -183,9 +191,9 @@ __device__ __forceinline__ i32x8 join(i32x4 lo, i32x4 hi) {
 // Unit n -> ring entry n % kRing: two A fragments (32 B per lane each, as two
 // lane-linear 16-B halves) and, for an encoding k-step, the B fragment.
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing]) {
-  const int slot = (n / kChunkUnits) % kSlots;
-  const unsigned addr = slot < kLoSlots ? cx.ring_addr : cx.ring_hi_addr;
-  const int off = (slot < kLoSlots ? slot : 0) * kChunkB + (n % kChunkUnits) * kUnitB;
+  const int s0 = (n / kChunkUnits) % kSlots;                   // the slot at rotation 0
+  const unsigned addr = s0 < 2 ? cx.ring_lo : cx.ring_hi;
+  const int off = s0 * kChunkB + (n % kChunkUnits) * kUnitB;
 #pragma unroll
   for (int o2 = 0; o2 < 2; ++o2)
     ra[n % kRing][o2] = join(ds_read_b128<i32x4>(addr, off + o2 * 2048),
@@ -291,6 +299,52 @@ __device__ __forceinline__ void layer_fp8b(f32x16 (&acc)[8], i32x8 (&bin)[4], i3
   }
 }
 
+// This tile's sample inputs -> its encodings in the wave's own LDS slots (e4m3), and
+// for fused compositing the integral's network-independent inputs.
+template <bool kExplicit>
+__device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src, long p, long n_points,
+                                            bool fused) {
+  float x[3], d[3], pef[32], def[16];
+  float dist = 0.0f, zz = 0.0f;
+  if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
+  else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, fused, x, d, dist, zz);
+  pos_encode<true>(x[0], x[1], x[2], cx.h, pef);
+  dir_encode<true>(d[0], d[1], d[2], cx.h, def);
+  // raw coordinates (slots 30, 31 of half 0, slot 30 of half 1) clamped to the e4m3 range
+  pef[30] = __builtin_fminf(__builtin_fmaxf(pef[30], -kFp8Max), kFp8Max);
+  pef[31] = __builtin_fminf(__builtin_fmaxf(pef[31], -kFp8Max), kFp8Max);
+  i32x4* pe_dst = (i32x4*)(cx.lds + kLdsPeOff + cx.wave_u * 2048 + cx.lane * 16);
+  i32x4* de_dst = (i32x4*)(cx.lds + kLdsDeOff + cx.wave_u * 2048 + cx.lane * 16);
+  i32x4 w0, w1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w0[i] = cvt4(pef[4 * i], pef[4 * i + 1], pef[4 * i + 2], pef[4 * i + 3]);
+    w1[i] = cvt4(pef[16 + 4 * i], pef[16 + 4 * i + 1], pef[16 + 4 * i + 2], pef[16 + 4 * i + 3]);
+  }
+  pe_dst[0] = w0;
+  pe_dst[64] = w1;                                   // +1024 B: the second 16-B half
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w0[i] = cvt4(def[4 * i], def[4 * i + 1], def[4 * i + 2], def[4 * i + 3]);
+  de_dst[0] = w0;
+  de_dst[64] = i32x4{0, 0, 0, 0};                    // direction slots 16..31: padding
+  if (!kExplicit && fused && cx.h == 0)
+    *(f32x2_t*)(cx.lds + kLdsSegOff + (cx.wave_u * kSamplesPerWave + (cx.lane & 31)) * 8) = f32x2_t{dist, zz};
+}
+
+// A tile's outputs, stored after the next tile's first seam: vmcnt counts stores
+// together with the LDS-DMA in issue order, so a store issued at the tile's end
+// would make that seam's vmcnt(0) wait for it as well.
+struct Pending {
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};   // (sigma, r, g, b) or half of a segment record
+  long idx = -1;                          // into out, or into seg (as f32x4); -1: none
+  float wl = 0.f;
+  long widx = -1;                         // into wloc; -1: none
+};
+__device__ __forceinline__ void store_pending(const Pending& pd, f32x4* out, float* wloc) {
+  if (pd.idx >= 0) out[pd.idx] = pd.v;
+  if (pd.widx >= 0) wloc[pd.widx] = pd.wl;
+}
+
 template <bool kExplicit>
 __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __restrict__ blob,
                                                               const float* __restrict__ prm_g, SampleSrc src,
@@ -301,139 +355,137 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const unsigned base = lds_addr(lds);
-  const Ctx cx{blob, lds, wave_u, lane, h,
-               base + lane * 16,
-               base + kLdsPeOff + wave_u * 2048 + lane * 16,
-               base + kLdsParamOff + h * 64,
-               base + kLdsScaleOff + lane * 8,
-               base + kLoSlots * kChunkB + lane * 16,
-               kLagOn && wave_u >= kWaves / 2 ? 1 : 0};
-  const long p = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
+  const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const bool fused = !kExplicit && seg != nullptr;
+  f32x4* const dst = fused ? seg : out;
+  Ctx cx0{blob, lds, base, wave_u, lane, h,
+          base + kLdsRingOff + lane * 16, base + kLdsRingOff + lane * 16,
+          base + kLdsPeOff + wave_u * 2048 + lane * 16,
+          base + kLdsParamOff + h * 64,
+          base + kLdsScaleOff + lane * 8,
+          0, wave_u >= kWaves / 2 ? 1 : 0};
 
-#pragma unroll
-  for (int g = 0; g < kSlots - 1 - kLagOn; ++g) stage_chunk(cx, g);
+  // The stream's first two chunks, and the parameters and row scales, once per workgroup.
+  stage_chunk(cx0, 0);
+  stage_chunk(cx0, 1);
   for (int i = threadIdx.x; i < kParamFloats / 4; i += kThreads)
     ((f32x4*)(lds + kLdsParamOff))[i] = ((const f32x4*)prm_g)[i];
   for (int i = threadIdx.x; i < kFp8ScaleBytes / 16; i += kThreads)
     ((f32x4*)(lds + kLdsScaleOff))[i] = ((const f32x4*)(blob + kFp8ScaleOff))[i];
-  {
-    float x[3], d[3], pef[32], def[16];
-    float dist = 0.0f, zz = 0.0f;
-    if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
-    else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, seg != nullptr, x, d, dist, zz);
-    pos_encode<true>(x[0], x[1], x[2], h, pef);
-    dir_encode<true>(d[0], d[1], d[2], h, def);
-    // raw coordinates (slots 30, 31 of half 0, slot 30 of half 1) clamped to the e4m3 range
-    pef[30] = __builtin_fminf(__builtin_fmaxf(pef[30], -kFp8Max), kFp8Max);
-    pef[31] = __builtin_fminf(__builtin_fmaxf(pef[31], -kFp8Max), kFp8Max);
-    i32x4* pe_dst = (i32x4*)(lds + kLdsPeOff + wave_u * 2048 + lane * 16);
-    i32x4* de_dst = (i32x4*)(lds + kLdsDeOff + wave_u * 2048 + lane * 16);
-    i32x4 w0, w1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      w0[i] = cvt4(pef[4 * i], pef[4 * i + 1], pef[4 * i + 2], pef[4 * i + 3]);
-      w1[i] = cvt4(pef[16 + 4 * i], pef[16 + 4 * i + 1], pef[16 + 4 * i + 2], pef[16 + 4 * i + 3]);
-    }
-    pe_dst[0] = w0;
-    pe_dst[64] = w1;                                   // +1024 B: the second 16-B half
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w0[i] = cvt4(def[4 * i], def[4 * i + 1], def[4 * i + 2], def[4 * i + 3]);
-    de_dst[0] = w0;
-    de_dst[64] = i32x4{0, 0, 0, 0};                    // direction slots 16..31: padding
-    if (!kExplicit && seg != nullptr) {                // the integral's network-independent inputs
-      if (h == 0) *(f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane & 31)) * 8) = f32x2_t{dist, zz};
-    }
-  }
-  wait_vmcnt(kGldsPerStage * (kSlots - 2 - kLagOn));   // chunk 0 landed (own pieces)
-  __syncthreads();
-  if (kLagOn && cx.lag) {
-    // the lagging half's extra seam (barrier instance 0): its pieces of chunk 1
-    // landed, then chunk kSlots-2 staged, as the leading half does at its seam 0
-    wait_vmcnt(kGldsPerStage * (kSlots - 4));
-    compiler_fence();
-    __builtin_amdgcn_s_barrier();
-    compiler_fence();
-    stage_chunk(cx, kSlots - 2);
-  }
-  i32x8 ra[kRing][2], rb[kRing];
-#pragma unroll
-  for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
-
-  f32x16 acc[8];
-  u32x4 hb[8];
-  // two fragment sets: layer l reads one while it fills the other for l+1
-  i32x8 bA[4], bB[4];
-  layer_fp8b<L0>(acc, bB, bA, ra, rb, hb, cx);
-  layer_fp8b<L1>(acc, bA, bB, ra, rb, hb, cx);
-  layer_fp8b<L2>(acc, bB, bA, ra, rb, hb, cx);
-  layer_fp8b<L3>(acc, bA, bB, ra, rb, hb, cx);
-  layer_fp8b<L4>(acc, bB, bA, ra, rb, hb, cx);   // skip: [x, pe] (nerf.py:109-110)
-  layer_fp8b<L5>(acc, bA, bB, ra, rb, hb, cx);
-  layer_fp8b<L6>(acc, bB, bA, ra, rb, hb, cx);
-  layer_fp8b<L7>(acc, bA, bB, ra, rb, hb, cx);
-  layer_fp8b<C0>(acc, bB, bA, ra, rb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
-  i32x8 (&bh)[4] = bB;                                   // C0's input: the density k-steps
-
-  // Heads (nerf.py:114, 123-129) as one MFMA tile: row 3 density (fp8 k-steps
-  // over bh, C0's input), rows 0-2 colour (bf16
-  // k-steps over hb, C0's output; tiles 2, 3 converted during the density units).
   const float* prm = (const float*)(lds + kLdsParamOff);
-  f32x16 hacc = f32x16{};
-  if (h == 0) {
-    hacc[0] = prm[kC1B];
-    hacc[1] = prm[kC1B + 1];
-    hacc[2] = prm[kC1B + 2];
-    hacc[3] = prm[kSigB];
-  }
-  int dsa = 127;
-#pragma unroll
-  for (int i = 0; i < kFp8HeadUnits; ++i) {
-    const int n = kFp8Units + i;
-    seam_before(cx, n);
-    if (i == 0) dsa = int(ds_read_b64(cx.scale_addr, (kNumMfmaLayers * 4) * 512)[0]);
-    if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
-    wait_lgkm(lgkm_for_unit(n));
-    if (i < kFp8DensityUnits) {
-#pragma unroll
-      for (int o2 = 0; o2 < 2; ++o2)
-        hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
-                                                               0, 127);
-#pragma unroll
-      for (int m = 0; m < 16; ++m)
-        if (m / 8 == i) colour_dword(acc, 2, m, hb);
+  Pending pd;
+
+#pragma unroll 1
+  for (long tile = blockIdx.x, it = 0; tile < n_tiles; tile += gridDim.x, ++it) {
+    // an opaque per-tile copy of the stream base: otherwise the 34 chunk addresses
+    // (blob + constant) are hoisted out of the tile loop and held in SGPRs
+    Ctx cx = cx0;
+    asm volatile("" : "+s"(cx.blob));
+    cx.rot = int(it & 1) * 2;
+    cx.ring_lo = cx0.ring_lo + unsigned(cx.rot * kChunkB);
+    cx.ring_hi = cx0.ring_hi - unsigned(cx.rot * kChunkB);
+    const long p = (tile * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
+    // this tile's encodings into the wave's own slots (its reads of the previous
+    // tile's were consumed by that tile's MFMAs)
+    encode_tile<kExplicit>(cx, src, p, n_points, fused);
+    if (it == 0) {
+      // barrier instance 0 publishes chunk 0 (and the parameters); the lagging half
+      // then takes its seam for chunk 0 (instance 1, staging chunk 2)
+      wait_vmcnt(kGldsPerStage);                     // own pieces of chunk 0 (chunk 1 may be in flight)
+      __syncthreads();
+      if (cx.lag) seam(cx, 0);
     } else {
+      seam(cx, 0);
+      store_pending(pd, dst, wloc);                  // the previous tile's outputs
+    }
+    i32x8 ra[kRing][2], rb[kRing];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const i32x8 a8 = ra[n % kRing][k >> 1];
-        const i32x4 a4 = (k & 1) ? i32x4{a8[4], a8[5], a8[6], a8[7]} : i32x4{a8[0], a8[1], a8[2], a8[3]};
-        hacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4),
-                                                        __builtin_bit_cast(bf16x8, hb[4 * (i - kFp8DensityUnits) + k]),
-                                                        hacc, 0, 0, 0);
+    for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
+
+    f32x16 acc[8];
+    u32x4 hb[8];
+    // two fragment sets: layer l reads one while it fills the other for l+1
+    i32x8 bA[4], bB[4];
+    layer_fp8b<L0>(acc, bB, bA, ra, rb, hb, cx);
+    layer_fp8b<L1>(acc, bA, bB, ra, rb, hb, cx);
+    layer_fp8b<L2>(acc, bB, bA, ra, rb, hb, cx);
+    layer_fp8b<L3>(acc, bA, bB, ra, rb, hb, cx);
+    layer_fp8b<L4>(acc, bB, bA, ra, rb, hb, cx);   // skip: [x, pe] (nerf.py:109-110)
+    layer_fp8b<L5>(acc, bA, bB, ra, rb, hb, cx);
+    layer_fp8b<L6>(acc, bB, bA, ra, rb, hb, cx);
+    layer_fp8b<L7>(acc, bA, bB, ra, rb, hb, cx);
+    layer_fp8b<C0>(acc, bB, bA, ra, rb, hb, cx);   // [x, PE4(d)] (nerf.py:117-121)
+    i32x8 (&bh)[4] = bB;                           // C0's input: the density k-steps
+
+    // Heads (nerf.py:114, 123-129) as one MFMA tile: row 3 density (fp8 k-steps
+    // over bh, C0's input), rows 0-2 colour (bf16 k-steps over hb, C0's output;
+    // tiles 2, 3 converted during the density units).
+    f32x16 hacc = f32x16{};
+    if (h == 0) {
+      hacc[0] = prm[kC1B];
+      hacc[1] = prm[kC1B + 1];
+      hacc[2] = prm[kC1B + 2];
+      hacc[3] = prm[kSigB];
+    }
+    int dsa = 127;
+#pragma unroll
+    for (int i = 0; i < kFp8HeadUnits; ++i) {
+      const int n = kFp8Units + i;
+      seam_before(cx, n);
+      if (i == 0) dsa = int(ds_read_b64(cx.scale_addr, (kNumMfmaLayers * 4) * 512)[0]);
+      if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      wait_lgkm(lgkm_for_unit(n));
+      if (i < kFp8DensityUnits) {
+#pragma unroll
+        for (int o2 = 0; o2 < 2; ++o2)
+          hacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][o2], bh[2 * i + o2], hacc, 0, 0, 0, dsa,
+                                                                 0, 127);
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if (m / 8 == i) colour_dword(acc, 2, m, hb);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const i32x8 a8 = ra[n % kRing][k >> 1];
+          const i32x4 a4 = (k & 1) ? i32x4{a8[4], a8[5], a8[6], a8[7]} : i32x4{a8[0], a8[1], a8[2], a8[3]};
+          hacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4),
+                                                          __builtin_bit_cast(bf16x8, hb[4 * (i - kFp8DensityUnits) + k]),
+                                                          hacc, 0, 0, 0);
+        }
       }
     }
+    // the sample index again, from the lane id recounted by v_mbcnt: keeping the
+    // 64-bit p (or the lane id) live through the layers costs a spill, and its
+    // reload a vmcnt(0) drain of the weight stream
+    const int lane_o = int(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+    const long p_o = (tile * kWaves + wave_u) * kSamplesPerWave + (lane_o & 31);
+    const f32x4 res{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
+    pd = Pending{};
+    if (fused) {                                       // fused compositing: one record per segment
+      const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane_o & 31)) * 8);
+      float wl;
+      pd.v = seg_composite(res, in[0], in[1], lane_o, wl);
+      const long first = p_o - (lane_o & 31);
+      if (first < n_points && lane_o < 2) pd.idx = (first / kSamplesPerWave) * 2 + lane_o;
+      if (wloc != nullptr && p_o < n_points && h == 0) {
+        pd.wl = wl;
+        pd.widx = p_o;
+      }
+    } else if (p_o < n_points && h == 0) {
+      pd.v = res;
+      pd.idx = p_o;
+    }
   }
-  if (kLagOn && !cx.lag) {
-    // the leading half's matching barrier for the lagging half's last seam
+  // the leading half's matching barrier for the lagging half's last seam
+  if (!cx0.lag) {
     compiler_fence();
     __builtin_amdgcn_s_barrier();
     compiler_fence();
   }
-  // the sample index again, from the lane id recounted by v_mbcnt: keeping the
-  // 64-bit p (or the lane id) live through the layers costs a spill, and its
-  // reload a vmcnt(0) drain of the weight stream
-  const int lane_o = int(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
-  const long p_o = (long(blockIdx.x) * kWaves + wave_u) * kSamplesPerWave + (lane_o & 31);
-  const f32x4 res{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
-  if (!kExplicit && seg != nullptr) {                  // fused compositing: one record per segment
-    const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane_o & 31)) * 8);
-    float wl;
-    const f32x4 rec = seg_composite(res, in[0], in[1], lane_o, wl);
-    const long first = p_o - (lane_o & 31);
-    if (first < n_points && lane_o < 2) seg[(first / kSamplesPerWave) * 2 + lane_o] = rec;
-    if (wloc != nullptr && p_o < n_points && h == 0) wloc[p_o] = wl;
-  } else if (p_o < n_points && h == 0) {
-    out[p_o] = res;
-  }
+  store_pending(pd, dst, wloc);
+  // the stream ran two chunks into a tile that does not exist: let them land
+  // before the workgroup's LDS is released
+  wait_vmcnt(0);
 }
 
 }  // namespace
@@ -441,7 +493,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
 hipError_t launch_mlp_fp8(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
                           bool explicit_points, hipStream_t stream, float* seg, float* wloc) {
   if (n_points <= 0) return hipSuccess;
-  const long blocks = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
   if (explicit_points)

@@ -17,7 +17,7 @@
 //
 // Structure: mlp_bf16.hip's (transposed Linear, accumulators become the next
 // layer's B fragments, quarter schedule, LDS ring filled by LDS-DMA with one
-// barrier per chunk, persistent tiles, asm fragment reads with counted waits),
+// barrier per chunk, persistent tiles, compiler-counted fragment reads),
 // with one wave per SIMD: a lane holds the layer's 8 accumulator tiles (128)
 // and the previous and next layers' hi and lo fragments (4 x 64), which only
 // fits in the 512-entry register file of a single wave (accumulators in AGPRs).
