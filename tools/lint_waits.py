@@ -1,10 +1,12 @@
 """Lint the counted waits of the MFMA kernels in an emitted gfx950 listing (.s).
 
-The MLP kernels issue their LDS fragment reads, LDS-DMA weight pieces and waits from
-inline asm with compile-time counts (mlp_x3.h, mlp_bf16.hip, mlp_fp8.hip: a unit table
-decides each `s_waitcnt lgkmcnt(N)`).  A count that is right only for one instruction
-schedule is a silent wrong-output bug, so this checks the listing the library is built
-from, instruction by instruction:
+The MLP kernels issue their LDS-DMA weight pieces from inline asm, which the compiler's
+waitcnt pass does not see, and rounds 1-3 also issued the LDS fragment reads from asm with
+compile-time `s_waitcnt lgkmcnt(N)` counts (the NERF_ASM_LDS_READS=1 lab form today).  A
+count that is right only for one instruction schedule, or an asm result the register
+allocator copies before its wait (what this lint found in round 4), is a silent
+wrong-output bug, so this checks the listing the library is built from, instruction by
+instruction:
 
   * every register written by a `ds_read*` (lgkmcnt) or a vector-memory load to registers
     (`global_load*` / `buffer_load*` without `lds`, vmcnt) is pending until a wait retires
