@@ -457,8 +457,8 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
     tr.set_profiling(False)
     losses.append(float(step(4 + n_steps)[0].item()))
     st = {k: float(np.mean([s[k] for s in stages])) for k in stages[0]}
-    # the same step with the forward on the split-bf16 MFMA (precision "bf16x3"), from the
-    # parameters as they now stand
+    # the same step with the forward and the backward-data chain on the split-bf16 MFMA
+    # (precision "bf16x3"), from the parameters as they now stand
     tr.set_precision("bf16x3")
     for i in range(2):
         step(5 + n_steps + i)
@@ -477,9 +477,10 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
     tr.set_precision("fp32")
     x3 = {"ms_per_step": 1e3 * dt_x3, "rays_per_s": TRAIN_RAYS / dt_x3,
           "stage_ms_rank0": {k: float(np.mean([s[k] for s in stages_x3])) for k in stages_x3[0]},
-          "note": "precision 'bf16x3': the forward on the split-bf16 MFMA (mlp_bf16x3.hip's kernel with the "
-                  "rows and ReLU bits the backward reads); gradients as close to the float64 step as the "
-                  "reference's fp32 step (tests/test_gpu_train.py); the default line above is fp32"}
+          "note": "precision 'bf16x3': the forward (mlp_bf16x3.hip's kernel with the rows and ReLU bits the "
+                  "backward reads) and the backward-data chain (train_bwd_x3.hip) on the split-bf16 MFMA; "
+                  "gradients as close to the float64 step as the reference's fp32 step "
+                  "(tests/test_gpu_train.py); the default line above is fp32"}
     # per-kernel rates in the unit each kernel is bound by: the fused forward and the
     # backward-data chain on the f32 MFMA, the weight gradients (split-bf16 MFMA) on HBM
     samples = (int(TRAIN_RAYS) // world + (1 if rank < TRAIN_RAYS % world else 0)) * (cfg["n_coarse"] + cfg["n_fine"])

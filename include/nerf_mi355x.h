@@ -317,11 +317,11 @@ int nerf_trainer_write(nerf_trainer* tr, int what, int net, const float* const* 
 int nerf_trainer_set_schedule(nerf_trainer* tr, long steps, double lr);
 /* The forward's arithmetic (the reference trains in fp32; no reference counterpart):
  * NERF_FP32 (default) the f32 MFMA, gradients at the fp32 ReLU-flip floor of the reference's;
- * NERF_BF16X3 the split-bf16 MFMA (mlp_bf16x3.hip's kernel with the rows and ReLU bits the
- * backward reads), about 1.9x the forward's rate, gradients as close to the float64 step's
- * as the reference's own fp32 step (more ReLU flips against the fp32 reference, so further
- * from it: DESIGN.md section 10).  The backward-data chain stays fp32; the weight gradients
- * are split-bf16 in both. */
+ * NERF_BF16X3 the split-bf16 MFMA for the forward (mlp_bf16x3.hip's kernel with the rows and
+ * ReLU bits the backward reads) and, since round 4, the backward-data chain
+ * (train_bwd_x3.hip), gradients as close to the float64 step's as the reference's own fp32
+ * step (more ReLU flips against the fp32 reference, so further from it: DESIGN.md section
+ * 10).  The weight gradients are split-bf16 in both. */
 int nerf_trainer_set_precision(nerf_trainer* tr, int precision);
 /* Clip + Adam + schedule on the gradients as they stand (the update half of train_step). */
 int nerf_trainer_update(nerf_trainer* tr, void* stream);

@@ -56,6 +56,16 @@ struct X3TrainOut {
 };
 hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
                                    const X3TrainOut& o, hipStream_t stream);
+// The training backward-data chain on the split-bf16 MFMA (train_bwd_x3.hip): dZ_7 .. dZ_0
+// rows from the head backward's rows, the stored ReLU bits and the packed transposed
+// weights (train_x3_layout.h; packed from the flat parameters by train.hip).
+struct BwdX3Io {
+  const float* dhc;          // [P][132]: colour-0 pre-activation gradients (128), density (128)
+  const float* wsig;         // density weights in accumulator order [h][tile 8][16] (params blob)
+  const unsigned* mb[8];     // ReLU bits of H_0..H_7, [P][8]
+  float* dz[8];              // out: dZ_0..dZ_7 rows [P][256]
+};
+hipError_t launch_train_bwd_x3(const void* blob, long n_points, const BwdX3Io& io, hipStream_t stream);
 // Chains each ray's segment records into (rgb, depth) (nerf_device.h SegRecord).
 hipError_t launch_composite_segments(const float* seg, int n_rays, int n_segments, float* rgb_out, float* depth_out,
                                      hipStream_t stream, OutStrides os = {});

@@ -22,6 +22,7 @@
 #include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
+#include "train_x3_layout.h"
 
 namespace nerf {
 namespace {
@@ -1239,6 +1240,32 @@ __global__ void pack_x3_kernel(const float* __restrict__ params, unsigned short*
   out[long(2 * n) * kX3UnitElems + off] = __builtin_bit_cast(unsigned short, hi);
   out[long(2 * n + 1) * kX3UnitElems + off] = __builtin_bit_cast(unsigned short, lo);
 }
+
+// Flat parameters -> the split-bf16 weight stream of the backward-data chain
+// (train_bwd_x3.hip, train_x3_layout.h), both nets: unit n = (backward layer b, quarter q,
+// k-step u), element (tile-in-quarter o2, lane, j) = W[hid_bf16_feature(u, lane / 32, j)]
+// [32 (2q + o2) + lane % 32] of the colour-0 layer (b = 0, its 256 hidden columns) or trunk
+// layer 8 - b; its bf16 hi half into the unit's first 2 KiB, lo = bf16(w - hi) into the second.
+constexpr long kBwdX3Elems = long(kBwdX3Units) * kX3UnitElems;        // elements of the hi (or lo) halves
+constexpr long kBwdX3NetElems = kBwdX3BlobBytes / 2;
+__global__ void pack_bwd_x3_kernel(const float* __restrict__ params, unsigned short* __restrict__ blob) {
+  const long i = long(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= kBwdX3Elems) return;
+  const float* prm = params + blockIdx.y * kNetFloats;
+  unsigned short* out = blob + blockIdx.y * kBwdX3NetElems;
+  const int n = int(i / kX3UnitElems), off = int(i % kX3UnitElems);
+  const int lane = (off / 8) % 64, j = off % 8, o2 = off / 512;
+  int b = 0;
+  while (b + 1 < kBwdX3Layers && bwd_x3_unit_base(b + 1) <= n) ++b;
+  const int ku = bwd_x3_ksteps(b), r = n - bwd_x3_unit_base(b), q = r / ku, u = r % ku;
+  const int row = 32 * (2 * q + o2) + (lane & 31), f = hid_bf16_feature(u, lane >> 5, j);
+  const int l = bwd_x3_trunk_layer(b);
+  const float v = b == 0 ? prm[kFC0W + long(f) * kHeadK + row] : prm[w_off(l) + long(f) * kTrunkIn[l] + row];
+  const __bf16 hi = __bf16(v);
+  const __bf16 lo = __bf16(__fsub_rn(v, float(hi)));
+  out[long(2 * n) * kX3UnitElems + off] = __builtin_bit_cast(unsigned short, hi);
+  out[long(2 * n + 1) * kX3UnitElems + off] = __builtin_bit_cast(unsigned short, lo);
+}
 }  // namespace
 }  // namespace nerf
 
@@ -1254,7 +1281,8 @@ struct nerf_trainer {
   float* v = nullptr;
   float* gemmw = nullptr;    // [2][kGemmFloats]
   unsigned short* x3 = nullptr;   // [2][kX3NetElems]: split-bf16 blob of the forward
-  bool fwd_x3 = false;            // forward on the split-bf16 MFMA (nerf_trainer_set_precision)
+  unsigned short* bx3 = nullptr;  // [2][kBwdX3NetElems]: split-bf16 blob of the backward-data chain
+  bool fwd_x3 = false;            // forward and backward-data on the split-bf16 MFMA (nerf_trainer_set_precision)
   float* ztab = nullptr;     // coarse table [n_coarse], fine table [n_fine]
   float* scal = nullptr;     // [0] clip coefficient, then double sum-of-squares partials
   int* bad = nullptr;        // device flag: a select index out of range
@@ -1283,9 +1311,12 @@ namespace {
 hipError_t pack_operands(nerf_trainer* tr, hipStream_t s) {
   hipLaunchKernelGGL(relayout_kernel, dim3(blocks_for(kGemmFloats, 256), 2), dim3(256), 0, s, (const float*)tr->params,
                      tr->gemmw);
-  if (tr->fwd_x3)
+  if (tr->fwd_x3) {
     hipLaunchKernelGGL(pack_x3_kernel, dim3(blocks_for(kX3Elems, 256), 2), dim3(256), 0, s, (const float*)tr->params,
                        tr->x3);
+    hipLaunchKernelGGL(pack_bwd_x3_kernel, dim3(blocks_for(kBwdX3Elems, 256), 2), dim3(256), 0, s,
+                       (const float*)tr->params, tr->bx3);
+  }
   return hipGetLastError();
 }
 
@@ -1517,12 +1548,20 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   HIP_TRY(hipGetLastError());
   {
     // dZ_7 .. dZ_0 in one launch (the head's and layers 7..1's data gradients with the ReLU bits)
-    BwdIo io;
-    io.dhc = a.dhc;
-    for (int l = 0; l < 8; ++l) io.mb[l] = a.mb[l], io.dz[l] = a.dz[l];
-    hipLaunchKernelGGL(train_bwd_kernel, dim3(blocks_for(P, 4 * kSamplesPerWave)), dim3(256), 0, s,
-                       (const f32x4*)(gw + kBwdBlob), P, io);
-    HIP_TRY(hipGetLastError());
+    if (tr->fwd_x3) {
+      BwdX3Io io;
+      io.dhc = a.dhc;
+      io.wsig = gw + kPrmBlob + kSigW;
+      for (int l = 0; l < 8; ++l) io.mb[l] = a.mb[l], io.dz[l] = a.dz[l];
+      HIP_TRY(launch_train_bwd_x3(tr->bx3 + net * kBwdX3NetElems, P, io, s));
+    } else {
+      BwdIo io;
+      io.dhc = a.dhc;
+      for (int l = 0; l < 8; ++l) io.mb[l] = a.mb[l], io.dz[l] = a.dz[l];
+      hipLaunchKernelGGL(train_bwd_kernel, dim3(blocks_for(P, 4 * kSamplesPerWave)), dim3(256), 0, s,
+                         (const f32x4*)(gw + kBwdBlob), P, io);
+      HIP_TRY(hipGetLastError());
+    }
   }
   if ((rc = mark(4)) != NERF_OK) return rc;
   {
@@ -1660,6 +1699,7 @@ int nerf_trainer_create(int device, const nerf_train_config* cfg, const float* c
   if (hipMalloc((void**)&tr->gemmw, sizeof(float) * 2 * kGemmFloats) != hipSuccess ||
       hipMalloc((void**)&tr->x3, sizeof(unsigned short) * 2 * kX3NetElems) != hipSuccess ||
       hipMemset(tr->x3, 0, sizeof(unsigned short) * 2 * kX3NetElems) != hipSuccess ||
+      hipMalloc((void**)&tr->bx3, sizeof(unsigned short) * 2 * kBwdX3NetElems) != hipSuccess ||
       hipMalloc((void**)&tr->ztab, sizeof(float) * 2048) != hipSuccess ||
       hipMalloc((void**)&tr->scal, sizeof(float) * (4 + 2 * kSqBlocks)) != hipSuccess ||
       hipMalloc((void**)&tr->bad, sizeof(int)) != hipSuccess)
@@ -1707,6 +1747,7 @@ void nerf_trainer_destroy(nerf_trainer* tr) {
     if (p) (void)hipFree(p);
   if (tr->bad) (void)hipFree(tr->bad);
   if (tr->x3) (void)hipFree(tr->x3);
+  if (tr->bx3) (void)hipFree(tr->bx3);
   for (auto& e : tr->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {tr->done, tr->fork, tr->join})

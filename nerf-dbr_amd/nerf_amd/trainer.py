@@ -121,8 +121,9 @@ class MI355XTrainer:
                                                ctypes.byref(h)))
         del kc, kf
         self._h = h
-        # the forward's arithmetic ("fp32": the reference's; "bf16x3": split bf16, faster,
-        # gradients as close to the float64 step as fp32's; include/nerf_mi355x.h)
+        # the forward's and backward-data chain's arithmetic ("fp32": the reference's;
+        # "bf16x3": split bf16, faster, gradients as close to the float64 step as fp32's;
+        # include/nerf_mi355x.h)
         self.precision = "fp32"
         try:
             self.set_precision(str(c.get("precision", "fp32")))
@@ -279,8 +280,9 @@ class MI355XTrainer:
         return int(self.lib.nerf_trainer_steps(self._h))
 
     def set_precision(self, precision: str) -> None:
-        """The forward's arithmetic: "fp32" (the reference's) or "bf16x3" (split bf16 on the
-        bf16 MFMA; nerf_trainer_set_precision in include/nerf_mi355x.h)."""
+        """The arithmetic of the forward and the backward-data chain: "fp32" (the reference's)
+        or "bf16x3" (split bf16 on the bf16 MFMA; nerf_trainer_set_precision in
+        include/nerf_mi355x.h)."""
         if precision not in ("fp32", "bf16x3"):
             raise ValueError(f"precision {precision!r}: 'fp32' or 'bf16x3'")
         rt._check(self.lib.nerf_trainer_set_precision(self._h, rt.PRECISIONS[precision]))

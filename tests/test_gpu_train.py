@@ -418,8 +418,8 @@ def test_cli_trains_then_benchmarks(tmp_path, monkeypatch):
 
 
 def test_train_bf16x3_forward_as_close_to_float64_as_fp32(fx):
-    """precision "bf16x3" (the forward on the split-bf16 MFMA): its rounding (~2^-17 per
-    product) flips more ReLUs than fp32's, so it sits further from the fp32 reference
+    """precision "bf16x3" (the forward and, since round 4, the backward-data chain on the
+    split-bf16 MFMA): its rounding (~2^-17 per product) flips more ReLUs than fp32's, so it sits further from the fp32 reference
     (up to 5.8e-3 normwise) but, measured against the float64 step, every gradient is as
     close as the reference's own fp32 step: GPU-vs-f64 <= 2 x fp32-vs-f64 + 1e-5 per tensor
     (measured: the GPU closer on 31 of 44 tensors); loss within 1e-5 of float64's."""

@@ -16,7 +16,21 @@ def fx(golden):
 @pytest.fixture(scope="module")
 def run(fx):
     """The oracle fed the reference's recorded draws: per-step losses and lrs, the
-    clipped gradients after step 1 and the parameters after step 3."""
+    clipped gradients after step 1 and the parameters after step 3.  torch's CPU GEMMs
+    split their reductions by thread, so the bit-exact comparison runs with the 8 threads
+    the fixture was generated with (this container's CPUs; an OMP_NUM_THREADS=2 run sums
+    density_head.weight's gradient in another order)."""
+    import torch
+
+    prev = torch.get_num_threads()
+    torch.set_num_threads(8)
+    try:
+        return _run(fx)
+    finally:
+        torch.set_num_threads(prev)
+
+
+def _run(fx):
     sd_c, sd_f = W.synthetic_models(0)
     cfg = dict(T.TRAIN_CONFIG, n_rays=int(fx["n_rays"]))
     orc = T.TrainOracle(sd_c, sd_f, cfg)
