@@ -54,11 +54,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 NL_HD bool is_seam(int n) { return (n + kPf) % kChunkUnits == 0 && n + kPf < kUnits && n + kPf != 0; }
-NL_HD int unit_layer(int n) {
-  int b = 0;
-  while (b + 1 < kBwdX3Layers && bwd_x3_unit_base(b + 1) <= n) ++b;
-  return b;
-}
 // the first seam inside backward layer b (where the next layer's mask words are requested)
 NL_HD int first_seam_unit(int b) {
   int n = bwd_x3_unit_base(b);
@@ -181,10 +176,8 @@ NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) /
 NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
 
 struct TileIo {
-  long p_first, n_points;
-  bool valid;
-  long p;
-  float dsig;
+  long p_first, n_points;   // the wave's first sample, the launch's samples
+  float dsig;               // this lane's density gradient (the head backward's row[128])
 };
 
 // Backward layer B: reads the previous layer's fragments (ih/il), fills the next's (oh/ol);
@@ -266,9 +259,8 @@ __global__ __launch_bounds__(kThreads, 1) void train_bwd_x3_kernel(const char* _
     TileIo ti;
     ti.n_points = n_points;
     ti.p_first = (tile * kWaves + wave_u) * kSamplesPerWave;
-    ti.p = ti.p_first + (lane & 31);
-    ti.valid = ti.p < n_points;
-    const long pc = ti.valid ? ti.p : n_points - 1;
+    const long p = ti.p_first + (lane & 31);
+    const long pc = p < n_points ? p : n_points - 1;
     // the colour-0 layer's inputs: the head backward's dZ rows, in the B fragments' k order
     // (k-step u, half h: features 16u + 4h + 0..3 and 16u + 8 + 4h + 0..3)
     u32x4 aH[16], aL[16], bH[16], bL[16];
