@@ -492,6 +492,16 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
         kernels[key] = {"stage": stage, "ms": st[stage], "flop": f, "achieved": f / (st[stage] * 1e-3) / 1e12,
                         "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
                         "frac": f / (st[stage] * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"]}
+    # the bf16x3 step's forward and backward-data on the split-bf16 MFMA: three bf16 MFMAs
+    # per fp32 product, priced against the bf16 peak / 3
+    sx = x3["stage_ms_rank0"]
+    x3_kernels = {}
+    for key, stage in (("forward", "forward_gemm"), ("backward_data", "backward_data_gemm")):
+        f = 2.0 * GEMM_MACS_PER_SAMPLE[key] * samples
+        x3_kernels[key] = {"stage": stage, "ms": sx[stage], "flop": f, "achieved": f / (sx[stage] * 1e-3) / 1e12,
+                           "peak": PEAK_TFLOPS["bf16x3"], "unit": "TFLOP/s",
+                           "frac": f / (sx[stage] * 1e-3) / 1e12 / PEAK_TFLOPS["bf16x3"]}
+    x3["gemm_kernels_rank0"] = x3_kernels
     b = WGRAD_OPERAND_BYTES_PER_SAMPLE * samples
     kernels["weight_grad"] = {"stage": "weight_grad_gemm", "ms": st["weight_grad_gemm"], "bytes": b,
                               "achieved": b / (st["weight_grad_gemm"] * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",

@@ -122,6 +122,11 @@ constexpr int kWBufs = BK == 16 ? NERF_WG_BUFS : 2;   // LDS-DMA buffers in flig
 #define NERF_WGRAD_X3 1
 #endif
 constexpr bool kWgradX3 = NERF_WGRAD_X3;   // split-bf16 weight gradients (wgrad_tile_x3); 0: fp32 MFMA
+// precision NERF_BF16X3 also runs the backward-data chain on the split-bf16 MFMA
+// (train_bwd_x3.hip); 0: the fp32 chain (train_bwd_kernel) under both precisions
+#ifndef NERF_TRAIN_BWD_X3
+#define NERF_TRAIN_BWD_X3 1
+#endif
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -1548,7 +1553,7 @@ int net_pass(nerf_trainer* tr, int net, const float* rays_o, const float* rays_d
   HIP_TRY(hipGetLastError());
   {
     // dZ_7 .. dZ_0 in one launch (the head's and layers 7..1's data gradients with the ReLU bits)
-    if (tr->fwd_x3) {
+    if (tr->fwd_x3 && NERF_TRAIN_BWD_X3) {
       BwdX3Io io;
       io.dhc = a.dhc;
       io.wsig = gw + kPrmBlob + kSigW;

@@ -11,4 +11,4 @@ echo "train tests rc=$rc"; grep -E "^FAILED|passed|failed|\[train" $OUT/train_te
 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --width 160 --height 120 --spp 32 --cpu-seconds 0 --no-error-check --no-extras > $OUT/bench_train.json 2> $OUT/bench_train.err || { echo "bench rc=$?"; tail -20 $OUT/bench_train.err; exit 1; }
 python -c "
 import json; b=json.loads(open('$OUT/bench_train.json').read().strip().splitlines()[-1])['training']
-print('fp32', b['ms_per_step'], b['stage_ms_rank0']); x=b['bf16x3_forward']; print('bf16x3', x['ms_per_step'], x['stage_ms_rank0'])"
+print('fp32', b['ms_per_step'], b['stage_ms_rank0']); x=b['bf16x3_forward']; print('bf16x3', x['ms_per_step'], x['stage_ms_rank0'], x.get('gemm_kernels_rank0'))"
