@@ -91,6 +91,23 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
 #undef NERF_VM
 }
 
+// s_waitcnt vmcnt(k) for every k in [0, 63] (the gfx9 field), k a constant after unrolling;
+// wait_vmcnt above keeps its coarser table (values it lacks wait for everything).
+__device__ __forceinline__ void wait_vmcnt_exact(int k) {
+#define NERF_VX(N) else if (k == N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");
+  if (k <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  NERF_VX(1) NERF_VX(2) NERF_VX(3) NERF_VX(4) NERF_VX(5) NERF_VX(6) NERF_VX(7) NERF_VX(8)
+  NERF_VX(9) NERF_VX(10) NERF_VX(11) NERF_VX(12) NERF_VX(13) NERF_VX(14) NERF_VX(15) NERF_VX(16)
+  NERF_VX(17) NERF_VX(18) NERF_VX(19) NERF_VX(20) NERF_VX(21) NERF_VX(22) NERF_VX(23) NERF_VX(24)
+  NERF_VX(25) NERF_VX(26) NERF_VX(27) NERF_VX(28) NERF_VX(29) NERF_VX(30) NERF_VX(31) NERF_VX(32)
+  NERF_VX(33) NERF_VX(34) NERF_VX(35) NERF_VX(36) NERF_VX(37) NERF_VX(38) NERF_VX(39) NERF_VX(40)
+  NERF_VX(41) NERF_VX(42) NERF_VX(43) NERF_VX(44) NERF_VX(45) NERF_VX(46) NERF_VX(47) NERF_VX(48)
+  NERF_VX(49) NERF_VX(50) NERF_VX(51) NERF_VX(52) NERF_VX(53) NERF_VX(54) NERF_VX(55) NERF_VX(56)
+  NERF_VX(57) NERF_VX(58) NERF_VX(59) NERF_VX(60) NERF_VX(61) NERF_VX(62)
+  else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+#undef NERF_VX
+}
+
 // One lane-linear 1 KiB LDS-DMA piece per wave, in saddr form: 16 B per lane
 // from SGPR base (wave-uniform 64-bit) + a per-lane 32-bit VGPR offset to LDS
 // byte address lds_base + lane*16 (wave-uniform base in M0), so advancing

@@ -19,8 +19,8 @@
 //   * the ReLU of the forward is the mask of the stored bits (v_bfe_i32 of the bit, AND);
 //   * each layer's masked accumulators also leave as the fp32 dZ rows [P][256];
 //   * a layer's mask words (32 B per sample, 1 KiB per wave) arrive by one LDS-DMA piece
-//     issued at the previous layer's first seam, so the seams' vmcnt(0) covers them and no
-//     compiler-counted global load waits for the weight stream inside the loop.
+//     issued at the previous layer's first seam, so the seams' counted vmcnt covers them and
+//     no compiler-counted global load waits for the weight stream inside the loop.
 #include "nerf_asm.h"
 #include "nerf_device.h"
 #include "nerf_internal.h"
@@ -37,16 +37,27 @@ constexpr int kUnitB = kBwdX3UnitBytes;                               // hi 2 Ki
 constexpr int kChunkUnits = kBwdX3ChunkUnits;
 constexpr int kChunkB = kChunkUnits * kUnitB;                         // 16 KiB
 constexpr int kTotalChunks = kUnits / kChunkUnits;                    // 120
-constexpr int kSlots = 3;
+// 4 ring slots, each chunk staged 2 seams before it is needed: a seam's counted wait then
+// leaves the row stores of two chunk periods in flight (kVm); 3 slots left one
+#ifndef NERF_BWD_X3_SLOTS
+#define NERF_BWD_X3_SLOTS 4
+#endif
+constexpr int kSlots = NERF_BWD_X3_SLOTS;
 constexpr int kPf = 3;                                                // fragment prefetch distance (units)
 constexpr int kRing = kPf + 1;
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);              // 4 pieces per wave per chunk
 static_assert(kTotalChunks % kSlots == 0, "the stream runs on into the next tile: chunk g always uses slot g % kSlots");
 static_assert(kSlots * kChunkB <= 65536, "ring offsets fit the ds_read offset field");
 constexpr int kLdsMaskOff = kSlots * kChunkB;                         // [wave][buffer 2][1 KiB]
-constexpr int kLdsBytes = kLdsMaskOff + kWaves * 2 * 1024;
+// dZ row staging: a tile pair's masked values, [sample 32][64 floats] per wave, rows padded
+// to 272 B so the 16-B writes of a lane-half hit distinct banks
+constexpr int kRowPitch = 272;
+constexpr int kLdsRowOff = kLdsMaskOff + kWaves * 2 * 1024;
+constexpr int kLdsRowWaveB = kSamplesPerWave * kRowPitch;              // 8.5 KiB
+constexpr int kLdsBytes = kLdsRowOff + kWaves * kLdsRowWaveB;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 constexpr int kHeadLd = 132;                                          // dhc rows: colour-0 (128), density
-constexpr int kRows = 256;                                            // dZ rows
+constexpr int kRows = 256;                                            // dZ row length (floats)
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -61,12 +72,64 @@ NL_HD int first_seam_unit(int b) {
   return n;
 }
 
+// Conversion schedule of mlp_x3.h: one dword per unit.
+NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
+NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
+
+// Counted seam waits.  Inside the loop a wave issues three kinds of vector-memory op: the
+// weight stream's LDS-DMA pieces (at seams), one mask-word piece per layer (after the
+// layer's first seam) and its dZ row stores (one per converted dword pair).  vmcnt retires
+// them in issue order (CDNA4 counts stores too), so a seam needs only the pieces staged at
+// the previous seam: it waits until no more than the ops issued after them -- that interval's
+// mask piece and stores -- are outstanding, and a row store gets a whole chunk to complete
+// instead of stalling the next seam (vmcnt(0) there made the chain wait for HBM writes).
+constexpr int kFlushStores = kSamplesPerWave * 256 / (64 * 16);       // 8 row stores per tile pair
+struct VmTable {
+  int ops[kUnits];      // vector-memory ops unit body n issues after its seam
+  int younger[kUnits];  // at the seam of body n: ops issued since the previous seam's stage
+};
+constexpr VmTable make_vm_table() {
+  VmTable t{};
+  for (int n = 0; n < kUnits; ++n) {
+    int b = 0;
+    while (b + 1 < kBwdX3Layers && bwd_x3_unit_base(b + 1) <= n) ++b;
+    const int ku = bwd_x3_ksteps(b), r = n - bwd_x3_unit_base(b), q = r / ku, u = r % ku;
+    int c = 0;
+    if (b != 0 && q == 0 && u == dword_unit_in(15)) c += kFlushStores;    // the previous layer's tiles 6, 7
+    if (q >= 1 && u == dword_unit_out(ku, 15)) c += kFlushStores;          // this layer's tiles 2q-2, 2q-1
+    int first = bwd_x3_unit_base(b);
+    while (!is_seam(first)) ++first;
+    if (b + 1 < kBwdX3Layers && n == first) ++c;                        // the next layer's mask words
+    t.ops[n] = c;
+  }
+  // A tile's stage events: the tile top stages chunk kSlots-2 (chunks below it have landed:
+  // the top drains vmcnt), seam j stages chunk j + kSlots - 1; seam k needs chunk k + 1.
+  int seams[kUnits] = {};
+  int ns = 0;
+  for (int n = 0; n < kUnits; ++n)
+    if (is_seam(n)) seams[ns++] = n;
+  for (int k = 0; k < ns; ++k) {
+    const int j = k + 1 - (kSlots - 1);     // the seam that staged chunk k+1 (< 0: the tile top)
+    const int from = j < 0 ? 0 : seams[j];  // the bodies after that stage
+    // stages issued after it: the seams between; from the top, seams 0..k-1, and the top's own
+    // when chunk k+1 had landed before it
+    const int stages = j < 0 ? k + (k + 1 < kSlots - 2 ? 1 : 0) : k - j - 1;
+    int y = kGldsPerStage * stages;
+    for (int m = from; m < seams[k]; ++m) y += t.ops[m];
+    t.younger[seams[k]] = y;
+  }
+  return t;
+}
+constexpr VmTable kVm = make_vm_table();
+
 struct Ctx {
   const char* blob;
   unsigned lds_base;               // LDS byte address of the ring (lds[0])
   int wave_u, lane, h;
   unsigned ring_addr, mask_addr;   // mask_addr: this wave's 2 x 1 KiB of mask words + (lane & 31) * 32
   unsigned mask_dma;               // LDS byte address of this wave's mask buffers
+  unsigned row_w;                  // this lane's sample row in the wave's dZ staging block
+  unsigned row_r;                  // the flush's read address: sample lane / 16, piece lane % 16
 };
 
 // LDS destinations as integer LDS addresses (a generic char* destination costs a 64-bit
@@ -80,12 +143,13 @@ __device__ __forceinline__ void stage_chunk(const char* __restrict__ blob, int g
                  dst + unsigned(i * kThreads * 16));
 }
 
-// Seam before the prefetch reaches chunk g+1: the wave's pieces of g+1 (and anything else
-// it issued) landed, the barrier publishes g+1 and frees chunk g-1's slot, which takes g+2.
+// Seam before the prefetch reaches chunk g+1: the wave's pieces of g+1 landed (counted:
+// kVm), the barrier publishes g+1 and frees chunk g+2-kSlots's slot, which takes g+kSlots-1
+// (every wave finished reading that chunk: its last unit was consumed before this seam).
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if (!is_seam(n)) return;
   const int g = (n + kPf) / kChunkUnits - 1;
-  wait_vmcnt(0);
+  wait_vmcnt_exact(kVm.younger[n]);
   compiler_fence();
   __builtin_amdgcn_s_barrier();
   compiler_fence();
@@ -144,18 +208,18 @@ __device__ __forceinline__ float masked(float v, unsigned ws, int r) {
 
 // Dword pr (registers 2pr, 2pr+1) of output tile t: masked, split into the next layer's
 // fragments (k-step 2t + (pr >> 2), dword pr & 3), and -- with the previous dword's pair --
-// stored as one 16-B piece of the sample's dZ row (registers 4j..4j+3 are features
-// 32t + 8j + 4h + 0..3).
-// A lane past the last sample computes the last sample's values (its inputs are clamped to
-// it) and stores them to that sample's row: identical bytes, so the stores need no exec
-// branch.
-struct Sink {
-  float* row;      // dZ row of this lane's sample (clamped)
-  float keep[2];
+// written as one 16-B piece of the sample's dZ row into the wave's LDS staging block
+// (registers 4j..4j+3 are features 32t + 8j + 4h + 0..3; the block holds the tile pair
+// t & ~1, t | 1).  flush_rows then stores the block as whole 256-B row segments.
+struct Keep {
+  float v[2];
 };
-__device__ __forceinline__ void convert_dword(const f32x16& tile, int t, int pr, unsigned word, int h, u32x4& fhi,
-                                              u32x4& flo, Sink& sk, bool split) {
-  const unsigned ws = word >> (4 * h);
+__device__ __forceinline__ void lds_store16(unsigned addr, f32x4 v) {
+  *(__attribute__((address_space(3))) f32x4*)(uintptr_t)addr = v;
+}
+__device__ __forceinline__ void convert_dword(const f32x16& tile, int t, int pr, unsigned word, const Ctx& cx,
+                                              u32x4& fhi, u32x4& flo, Keep& kp, bool split) {
+  const unsigned ws = word >> (4 * cx.h);
   const float v0 = masked(tile[2 * pr], ws, 2 * pr), v1 = masked(tile[2 * pr + 1], ws, 2 * pr + 1);
   if (split) {
     unsigned hi, lo;
@@ -164,16 +228,34 @@ __device__ __forceinline__ void convert_dword(const f32x16& tile, int t, int pr,
     flo[pr & 3] = lo;
   }
   if (pr & 1) {
-    *(f32x4*)(sk.row + 32 * t + 8 * (pr >> 1) + 4 * h) = f32x4{sk.keep[0], sk.keep[1], v0, v1};
+#ifndef NERF_BWD_X3_ABLATE_NOSTORE   // timing-only lab build (no dZ rows): what the row stores cost
+    lds_store16(cx.row_w + unsigned(((t & 1) * 32 + 8 * (pr >> 1) + 4 * cx.h) * 4), f32x4{kp.v[0], kp.v[1], v0, v1});
+#else
+    asm volatile("" ::"v"(kp.v[0]), "v"(kp.v[1]), "v"(v0), "v"(v1));
+#endif
   } else {
-    sk.keep[0] = v0;
-    sk.keep[1] = v1;
+    kp.v[0] = v0;
+    kp.v[1] = v1;
   }
 }
-
-// Conversion schedule of mlp_x3.h: one dword per unit.
-NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
-NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
+// The staged tile pair (features f0 .. f0+63 of the wave's 32 samples) to the dZ rows: lane
+// l stores 16 B of sample 4i + l / 16, so one instruction writes four whole 256-B segments.
+// A sample past the last one is clamped to it (its values equal the last sample's).
+__device__ __forceinline__ void flush_rows(const Ctx& cx, float* __restrict__ dz, long p_first, long n_points, int f0) {
+#ifndef NERF_BWD_X3_ABLATE_NOSTORE
+#pragma unroll
+  for (int i = 0; i < kSamplesPerWave / 4; ++i) {
+    const f32x4 v = ds_read_b128<f32x4>(cx.row_r, i * 4 * kRowPitch);
+    long s = p_first + 4 * i + (cx.lane >> 4);
+    s = s < n_points ? s : n_points - 1;
+#ifdef NERF_BWD_X3_NT_STORES   // lab: streaming (non-temporal) row stores
+    __builtin_nontemporal_store(v, (f32x4*)(dz + s * kRows + f0 + 4 * (cx.lane & 15)));
+#else
+    *(f32x4*)(dz + s * kRows + f0 + 4 * (cx.lane & 15)) = v;
+#endif
+  }
+#endif
+}
 
 struct TileIo {
   long p_first, n_points;   // the wave's first sample, the launch's samples
@@ -186,12 +268,12 @@ struct TileIo {
 template <int B>
 __device__ __forceinline__ void layer_bwd(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
                                           u32x4 (&ol)[16], bf16x8 (&ra)[kRing][4], const Ctx& cx, const BwdX3Io& io,
-                                          const TileIo& ti, const u32x4 (&wc)[2], const u32x4 (&wp)[2], Sink& sk_prev,
-                                          Sink& sk) {
+                                          const TileIo& ti, const u32x4 (&wc)[2], const u32x4 (&wp)[2]) {
   constexpr int KU = bwd_x3_ksteps(B);
   constexpr int N0 = bwd_x3_unit_base(B);
   constexpr bool kConvertPrev = B != 0;
   constexpr bool kSplit = B != kBwdX3Layers - 1;     // the last layer's output feeds nothing
+  Keep kp;                                           // a dword pair's values until the next (odd) dword
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -226,13 +308,16 @@ __device__ __forceinline__ void layer_bwd(f32x16 (&acc)[8], u32x4 (&ih)[16], u32
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
-        if (kConvertPrev && q == 0 && u == dword_unit_in(m))
-          convert_dword(acc[6 + t], 6 + t, pr, wp[1][2 + t], cx.h, ih[2 * (6 + t) + (pr >> 2)],
-                        il[2 * (6 + t) + (pr >> 2)], sk_prev, true);
+        if (kConvertPrev && q == 0 && u == dword_unit_in(m)) {
+          convert_dword(acc[6 + t], 6 + t, pr, wp[1][2 + t], cx, ih[2 * (6 + t) + (pr >> 2)],
+                        il[2 * (6 + t) + (pr >> 2)], kp, true);
+          if (m == 15) flush_rows(cx, io.dz[8 - B], ti.p_first, ti.n_points, 192);   // the previous layer's dZ
+        }
         if (q >= 1 && u == dword_unit_out(KU, m)) {
           const int tt = 2 * q - 2 + t;
-          convert_dword(acc[tt], tt, pr, wc[tt >> 2][tt & 3], cx.h, oh[2 * tt + (pr >> 2)], ol[2 * tt + (pr >> 2)], sk,
+          convert_dword(acc[tt], tt, pr, wc[tt >> 2][tt & 3], cx, oh[2 * tt + (pr >> 2)], ol[2 * tt + (pr >> 2)], kp,
                         kSplit);
+          if (m == 15) flush_rows(cx, io.dz[7 - B], ti.p_first, ti.n_points, 64 * (q - 1));
         }
       }
     }
@@ -246,11 +331,14 @@ __global__ __launch_bounds__(kThreads, 1) void train_bwd_x3_kernel(const char* _
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const unsigned base = lds_addr(lds);
+  const unsigned rows = base + kLdsRowOff + wave_u * kLdsRowWaveB;
   const Ctx cx0{blob, base, wave_u, lane, h, base + lane * 16,
-                base + kLdsMaskOff + wave_u * 2048 + (lane & 31) * 32, base + kLdsMaskOff + wave_u * 2048};
+                base + kLdsMaskOff + wave_u * 2048 + (lane & 31) * 32, base + kLdsMaskOff + wave_u * 2048,
+                rows + (lane & 31) * kRowPitch, rows + (lane >> 4) * kRowPitch + (lane & 15) * 16};
   const long n_tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
-  stage_chunk(blob, 0, base, wave_u, lane);
+#pragma unroll
+  for (int g = 0; g < kSlots - 2; ++g) stage_chunk(blob, g, base, wave_u, lane);
 
 #pragma unroll 1
   for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -275,42 +363,41 @@ __global__ __launch_bounds__(kThreads, 1) void train_bwd_x3_kernel(const char* _
       ti.dsig = row[128];
     }
     request_masks(cx, io.mb[7], ti.p_first, n_points, 0);
-    // the tile's first seam: chunk 0 (staged by the last tile's seams, or the prologue)
-    // and the mask words landed; chunk 1 starts into its slot
+    // the tile's first seam: chunks 0 .. kSlots-3 (staged by the last tile's seams, or the
+    // prologue), the mask words and the last tile's row stores landed; chunk kSlots-2 starts
+    // into its slot
     wait_vmcnt(0);
     __syncthreads();
-    stage_chunk(cx.blob, 1, base, wave_u, lane);
+    stage_chunk(cx.blob, kSlots - 2, base, wave_u, lane);
     bf16x8 ra[kRing][4];
 #pragma unroll
     for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra);
     f32x16 acc[8];
     u32x4 w[2][2];
     read_masks(cx, 0, w[0]);
-    Sink s7{io.dz[7] + pc * kRows, {0.f, 0.f}}, s6{io.dz[6] + pc * kRows, {0.f, 0.f}};
-    Sink s5{io.dz[5] + pc * kRows, {0.f, 0.f}}, s4{io.dz[4] + pc * kRows, {0.f, 0.f}};
-    Sink s3{io.dz[3] + pc * kRows, {0.f, 0.f}}, s2{io.dz[2] + pc * kRows, {0.f, 0.f}};
-    Sink s1{io.dz[1] + pc * kRows, {0.f, 0.f}}, s0{io.dz[0] + pc * kRows, {0.f, 0.f}};
-    layer_bwd<0>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1], s7, s7);      // dZ_7 (mask: H_7)
+    layer_bwd<0>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1]);      // dZ_7 (mask: H_7)
     read_masks(cx, 1, w[1]);
-    layer_bwd<1>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0], s7, s6);      // dZ_6
+    layer_bwd<1>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0]);      // dZ_6
     read_masks(cx, 0, w[0]);
-    layer_bwd<2>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1], s6, s5);      // dZ_5
+    layer_bwd<2>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1]);      // dZ_5
     read_masks(cx, 1, w[1]);
-    layer_bwd<3>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0], s5, s4);      // dZ_4
+    layer_bwd<3>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0]);      // dZ_4
     read_masks(cx, 0, w[0]);
-    layer_bwd<4>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1], s4, s3);      // dZ_3
+    layer_bwd<4>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1]);      // dZ_3
     read_masks(cx, 1, w[1]);
-    layer_bwd<5>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0], s3, s2);      // dZ_2
+    layer_bwd<5>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0]);      // dZ_2
     read_masks(cx, 0, w[0]);
-    layer_bwd<6>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1], s2, s1);      // dZ_1
+    layer_bwd<6>(acc, bH, bL, aH, aL, ra, cx, io, ti, w[0], w[1]);      // dZ_1
     read_masks(cx, 1, w[1]);
-    layer_bwd<7>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0], s1, s0);      // dZ_0
+    layer_bwd<7>(acc, aH, aL, bH, bL, ra, cx, io, ti, w[1], w[0]);      // dZ_0
     // the last layer's tiles 6, 7 (no next layer to convert them in)
+    Keep kp;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int t = 6 + (m >> 3), pr = m & 7;
-      convert_dword(acc[t], t, pr, w[1][1][t & 3], h, aH[0], aL[0], s0, false);
+      convert_dword(acc[t], t, pr, w[1][1][t & 3], cx, aH[0], aL[0], kp, false);
     }
+    flush_rows(cx, io.dz[0], ti.p_first, n_points, 192);
   }
   // the stream ran into a tile that does not exist: let it land before the LDS is released
   wait_vmcnt(0);
