@@ -9,9 +9,9 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -q --timeout 200 --timeout-method thread > $OUT/train_tests.log 2>&1 || { echo "train tests rc=$?"; tail -20 $OUT/train_tests.log; exit 1; }
 tail -1 $OUT/train_tests.log
 cd /tmp
-for v in default nt nostore; do
+for v in default fwdplain; do
   lib=$GRAFT_REPO_ROOT/nerf-dbr_amd/nerf_amd/_lib/libnerf_mi355x.so
-  [ $v != default ] && lib=$GRAFT_REPO_ROOT/labx/libnerf_bwd$v.so
+  [ $v != default ] && lib=$GRAFT_REPO_ROOT/labx/libnerf_$v.so
   NERF_MI355X_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/prof_$v -o run \
     -- python3 $GRAFT_REPO_ROOT/tools/train_profile.py 5 bf16x3 > $OUT/prof_$v.log 2>&1 || { echo "prof $v rc=$?"; tail -5 $OUT/prof_$v.log; exit 1; }
   python3 -c "
