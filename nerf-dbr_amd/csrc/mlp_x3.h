@@ -74,6 +74,12 @@ constexpr int kLdsDeOff = kLdsPeOff + kWaves * kPeWaveB;
 constexpr int kLdsSegOff = kLdsDeOff + kWaves * kDeWaveB;            // fused compositing: (dist, z) per sample
 constexpr int kLdsBytes = kLdsSegOff + kWaves * kSamplesPerWave * 8;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+// Training forward only: a tile pair's ReLU'd rows staged per wave, [sample 32][64 floats] at
+// a 272-B pitch (conflict-free 16-B writes), stored as whole 256-B row segments
+constexpr int kRowPitch = 272;
+constexpr int kLdsRowOff = kLdsBytes;
+constexpr int kLdsBytesTrain = kLdsRowOff + kWaves * kSamplesPerWave * kRowPitch;
+static_assert(kLdsBytesTrain <= 160 * 1024, "LDS budget (training forward)");
 // ds_read offsets are 16 bits: slots below kLoSlots are read at ring_addr + offset,
 // the rest at ring_hi_addr (= ring_addr + kLoSlots * kChunkB) + offset
 constexpr int kLoSlots = 65536 / kChunkB < kSlots ? 65536 / kChunkB : kSlots;
@@ -353,7 +359,29 @@ struct TrainSink {
   long p;
   bool valid;
   unsigned bits[2];
+  long p_first;         // the wave's first sample
+  long n_points;
+  unsigned row_w;       // LDS: this lane's sample row in the wave's staging block
+  unsigned row_r;       // LDS: the flush's read address (sample lane / 16, piece lane % 16)
+  int lane;
 };
+__device__ __forceinline__ void lds_store16(unsigned addr, f32x4 v) {
+  *(__attribute__((address_space(3))) f32x4*)(uintptr_t)addr = v;
+}
+// The staged tile pair t0, t0+1 of layer l (features 32 t0 .. +63 of the wave's 32 samples)
+// to the rows: lane l stores 16 B of sample 4i + l / 16, four whole 256-B segments per
+// instruction, non-temporal for the 1-KiB h rows (read once, by the backward and the weight
+// gradients); a sample past the last is clamped to it (its values equal the last sample's).
+__device__ __forceinline__ void flush_rows(const TrainSink& sk, int l, int t0, int lane) {
+#pragma unroll
+  for (int i = 0; i < kSamplesPerWave / 4; ++i) {
+    const f32x4 v = ds_read_b128<f32x4>(sk.row_r, i * 4 * kRowPitch);
+    long s = sk.p_first + 4 * i + (lane >> 4);
+    s = s < sk.n_points ? s : sk.n_points - 1;
+    if (l < 8) __builtin_nontemporal_store(v, (f32x4*)(sk.o.h[l] + s * 256 + 32 * t0 + 4 * (lane & 15)));
+    else *(f32x4*)(sk.o.hc + s * 132 + 32 * t0 + 4 * (lane & 15)) = v;
+  }
+}
 template <bool kTrain>
 __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot, const f32x16& tile, int pr, int h) {
   if constexpr (kTrain) {
@@ -366,12 +394,11 @@ __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot
         if (sk.valid && h == 0) sk.o.mb[l][sk.p * 8 + t] = unsigned(sw[0]) | unsigned(sw[1]);
       }
     }
-    if (pr & 1) {
+    if (pr & 1) {   // registers 4j..4j+3 are features 32t + 8j + 4h + 0..3: into the staging block
       const int j = pr >> 1;
-      float* row = l < 8 ? sk.o.h[l] + sk.p * 256 : sk.o.hc + sk.p * 132;
-      if (sk.valid)
-        *(f32x4*)(row + 32 * t + 8 * j + 4 * h) =
-            f32x4{relu(tile[4 * j]), relu(tile[4 * j + 1]), relu(tile[4 * j + 2]), relu(tile[4 * j + 3])};
+      lds_store16(sk.row_w + unsigned(((t & 1) * 32 + 8 * j + 4 * h) * 4),
+                  f32x4{relu(tile[4 * j]), relu(tile[4 * j + 1]), relu(tile[4 * j + 2]), relu(tile[4 * j + 3])});
+      if (pr == 7 && (t & 1)) flush_rows(sk, l, t - 1, sk.lane);   // the pair's last dword
     }
   }
 }
@@ -430,7 +457,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
                                                              f32x4* __restrict__ seg, X3TrainOut tro,
                                                              int* __restrict__ range_flag) {
   typedef typename Op::frag F;
-  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) char lds[kTrain ? kLdsBytesTrain : kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
@@ -474,7 +501,9 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     const long p0 = (tile * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
     Ctx cx = cx0;
     asm volatile("" : "+s"(cx.blob));   // keep the 132 chunk addresses out of SGPRs across tiles
-    TrainSink sk{tro, p0, p0 < n_points, {0u, 0u}};
+    const unsigned rows = lds_base + kLdsRowOff + wave_u * kSamplesPerWave * kRowPitch;
+    TrainSink sk{tro, p0, p0 < n_points, {0u, 0u}, (tile * kWaves + wave_u) * kSamplesPerWave, n_points,
+                 rows + (lane & 31) * kRowPitch, rows + (lane >> 4) * kRowPitch + (lane & 15) * 16, lane};
 #ifdef NERF_X3_ABLATE_PE_ONCE   // timing-only lab build (wrong results): encodings of the first tile reused
     if (tile == blockIdx.x)
 #endif
