@@ -449,6 +449,48 @@ def test_train_bf16x3_forward_as_close_to_float64_as_fp32(fx):
     gpu.close()
 
 
+@pytest.mark.parametrize("n_rays,n_coarse,n_fine", [(37, 64, 128), (300, 24, 40), (3, 5, 7), (1, 8, 8)])
+def test_train_bf16x3_ragged_shapes_against_float64(n_rays, n_coarse, n_fine):
+    """The split kernels' partial tiles: sample counts that are not a multiple of a wave's
+    32 samples or a workgroup's 128 (the forward's staged row stores and the backward-data
+    chain's clamped duplicate stores past the last sample), down to one ray of 16 samples.
+    Against the float64 step as above, with an absolute allowance for the small batches'
+    cancellations (test_train_step_tiny_shapes: fp32 itself is 1e-4 off on the heads there):
+    GPU-vs-f64 <= 2 x fp32-vs-f64 + 2e-4 per tensor and for the loss (+1e-6 relative):
+    with one to three rays the fp32 step's own loss is 1e-5 - 8e-5 from float64's (measured
+    with the pre-staging build too: the same loss to the bit).  A lost or misplaced row
+    would be off by O(1) on its layer."""
+    rng = np.random.RandomState(200 + n_rays)
+    h, w = 20, 24
+    image = rng.rand(h, w, 3).astype(np.float32)
+    pose = _look_at([0.3, -3.5, 1.2])
+    sel = rng.permutation(h * w)[:n_rays]
+    tr = rng.rand(n_rays, n_coarse).astype(np.float32)
+    cfg = {"n_coarse": n_coarse, "n_fine": n_fine, "precision": "bf16x3"}
+    sd_c, sd_f = W.synthetic_models(0)
+    gpu, orc = _trainer(n_rays, cfg, (sd_c, sd_f))
+    batch = {"image": torch.from_numpy(image), "pose": torch.from_numpy(pose), "focal": 20.0}
+    loss = gpu.train_step(batch, select_inds=sel.astype(np.int32), t_rand=tr, update=False)
+    args = (image, pose, 20.0, sel, tr)
+    loss32 = orc.backward(*args)[0]
+    ocfg = dict(T.TRAIN_CONFIG, n_rays=n_rays, n_coarse=n_coarse, n_fine=n_fine)
+    loss64, g64 = T.step_grads_f64(sd_c, sd_f, *args, ocfg)
+    print(f"\n[train bf16x3 {n_rays}x({n_coarse}+{n_fine})] loss rel err GPU {abs(loss - loss64) / loss64:.3g}, "
+          f"fp32 {abs(loss32 - loss64) / loss64:.3g}")
+    assert abs(loss - loss64) <= 2.0 * abs(loss32 - loss64) + 1e-6 * abs(loss64), (loss, loss32, loss64)
+    worst = 0.0
+    for net in range(2):
+        gg, g32 = gpu.grads(net), orc.grads(net)
+        for k in T.PARAM_ORDER:
+            a, b, c = (np.asarray(x, np.float64).ravel() for x in (gg[k], g64[net][k], g32[k]))
+            nb = max(np.linalg.norm(b), 1e-300)
+            e_gpu, e32 = np.linalg.norm(a - b) / nb, np.linalg.norm(c - b) / nb
+            worst = max(worst, e_gpu)
+            assert e_gpu <= 2.0 * e32 + 2e-4, (net, k, e_gpu, e32)
+    print(f"\n[train bf16x3 {n_rays}x({n_coarse}+{n_fine})] worst GPU-vs-f64 {worst:.3g}")
+    gpu.close()
+
+
 def test_train_precision_switch_rejects_unknown():
     from nerf_amd.trainer import MI355XTrainer
 
