@@ -373,6 +373,9 @@ __device__ __forceinline__ void lds_store16(unsigned addr, f32x4 v) {
 // instruction, non-temporal for the 1-KiB h rows (read once, by the backward and the weight
 // gradients); a sample past the last is clamped to it (its values equal the last sample's).
 __device__ __forceinline__ void flush_rows(const TrainSink& sk, int l, int t0, int lane) {
+#ifdef NERF_X3_ABLATE_NOSTORE   // timing-only lab build (no rows): what the training rows cost
+  return;
+#endif
 #pragma unroll
   for (int i = 0; i < kSamplesPerWave / 4; ++i) {
     const f32x4 v = ds_read_b128<f32x4>(sk.row_r, i * 4 * kRowPitch);
@@ -391,7 +394,9 @@ __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot
       sk.bits[slot] = (pr == 0 ? 0u : sk.bits[slot]) | m;
       if (pr == 7) {
         const auto sw = __builtin_amdgcn_permlane32_swap(sk.bits[slot], sk.bits[slot], false, false);
+#ifndef NERF_X3_ABLATE_NOSTORE
         if (sk.valid && h == 0) sk.o.mb[l][sk.p * 8 + t] = unsigned(sw[0]) | unsigned(sw[1]);
+#endif
       }
     }
     if (pr & 1) {   // registers 4j..4j+3 are features 32t + 8j + 4h + 0..3: into the staging block
