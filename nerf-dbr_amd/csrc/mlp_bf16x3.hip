@@ -14,6 +14,7 @@ hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const Sample
 hipError_t launch_mlp_bf16x3_train(const void* blob, const float* params, const SampleSrc& src, long n_points,
                                    const X3TrainOut& o, hipStream_t stream) {
   if (n_points <= 0) return hipSuccess;
+  if (n_points >= (1L << 27)) return hipErrorInvalidValue;   // the ReLU-bit words' 32-bit byte offsets
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   hipLaunchKernelGGL((mlp_x3_kernel<false, true, OpBf16>), dim3(unsigned(blocks)), dim3(kThreads), 0, stream,

@@ -55,6 +55,10 @@ constexpr int kUnitB = 2 * kUnitBytes;                                // 4 KiB: 
 #ifndef NERF_X3_PF
 #define NERF_X3_PF 3
 #endif
+// counted seam waits in the training forward (needs NERF_X3_SLOTS=4; mlp_bf16x3.hip)
+#ifndef NERF_X3_TRAIN_COUNTED
+#define NERF_X3_TRAIN_COUNTED 0
+#endif
 constexpr int kChunkUnits = NERF_X3_CHUNK_UNITS;
 constexpr int kChunkB = kChunkUnits * kUnitB;                         // 16 KiB
 constexpr int kTotalChunks = (kUnits + kChunkUnits - 1) / kChunkUnits;   // 132
@@ -278,6 +282,56 @@ static_assert(!NERF_X3_SPREAD || !NERF_X3_REGSTAGE, "one staging form");
 static_assert(!NERF_X3_REGSTAGE || kSlots == 3, "register staging: chunk g+2 written at seam g into chunk g-1's slot");
 static_assert(!NERF_X3_SPREAD || (kGldsPerStage <= kChunkUnits && kSlots >= 4),
               "spread pieces land within a chunk, and need one chunk of slack at the next seam");
+// Training forward (kTrain): the seams' vmcnt waits are counted.  vmcnt retires vector-memory
+// operations in issue order, LDS-DMA pieces and stores alike; the chunk a seam publishes
+// (g + 1) was staged two seams earlier, so everything issued after that stage -- the
+// stage at the seam between (kGldsPerStage pieces) and the sink's row and ReLU-bit stores
+// of the bodies since -- may stay in flight.  A vmcnt(kGldsPerStage) wait (kSlots = 4)
+// would also drain every store issued since the last stage.  The store counts per unit
+// body mirror layer_x3 and the heads loop (every store is unconditional: samples past the
+// last are clamped to it); the tile top waits vmcnt(0), so a tile's first two seams count
+// from the tile top.
+constexpr int kFlushStores = kSamplesPerWave / 4;        // flush_rows: one 16-B store per 4 lanes' sample
+struct TrainVm {
+  int stores[kUnits];                                    // global stores of unit body n (after its seam)
+  int seam[kUnits];                                      // the seam wait before body n, if is_seam(n)
+};
+constexpr void add_sink_stores(TrainVm& t, int n, int l, int tile, int pr) {
+  if (pr != 7) return;
+  if (l < 8) t.stores[n] += 1;                           // the tile's ReLU-bit word
+  if (tile & 1) t.stores[n] += kFlushStores;             // the tile pair's rows
+}
+constexpr int dword_unit_out_c(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
+constexpr int dword_unit_in_c(int m) { return 2 + (m * 10) / 16; }
+constexpr TrainVm make_train_vm() {
+  TrainVm t{};
+  for (int L = 0; L < kNumMfmaLayers; ++L) {
+    const int KU = ksteps_bf16(L), NQ = out_tiles(L) / 2, N0 = bf16_unit_base(L);
+    for (int q = 0; q < NQ; ++q)
+      for (int u = 0; u < KU; ++u)
+        for (int m = 0; m < 16; ++m) {
+          const int n = N0 + q * KU + u, tt = m >> 3, pr = m & 7;
+          if (L != L0 && q == 0 && u == dword_unit_in_c(m)) add_sink_stores(t, n, L - 1, 6 + tt, pr);
+          if (q >= 1 && u == dword_unit_out_c(KU, m)) add_sink_stores(t, n, L, 2 * q - 2 + tt, pr);
+        }
+  }
+  for (int i = 0; i < kHeadUnits; ++i)
+    for (int m = 0; m < 16; ++m)
+      if (i < 8 && m / 2 == i) add_sink_stores(t, kHeadUnitBase + i, C0, 2 + (m >> 3), m & 7);
+  for (int n = 0; n < kUnits; ++n) {
+    if (!is_seam(n)) continue;
+    const int g = (n + kPf) / kChunkUnits - 1;
+    const int from = g >= 2 ? kChunkUnits * (g - 1) - kPf : 0;   // body of seam g - 2 (its stage precedes its stores)
+    int c = kGldsPerStage;                                        // the stage at seam g - 1 (or the tile top)
+    for (int k = from; k < n; ++k) c += t.stores[k];
+    t.seam[n] = c;
+  }
+  return t;
+}
+constexpr TrainVm kTrainVm = make_train_vm();
+static_assert(kSlots == 4 || !NERF_X3_TRAIN_COUNTED, "counted training seams: chunk g + 1 staged two seams ahead");
+
+template <bool kTrain = false>
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
   if (NERF_X3_SPREAD) {
 #pragma unroll
@@ -297,7 +351,8 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
     load_chunk_regs(cx, (g + kStageAhead + 1) % kTotalChunks);
     return;
   }
-  wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
+  if (kTrain && NERF_X3_TRAIN_COUNTED) wait_vmcnt_exact(kTrainVm.seam[n]);
+  else wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
   compiler_fence();
 #ifndef NERF_X3_ABLATE_NOBARRIER   // timing-only lab build (wrong results): no seam barriers
   __builtin_amdgcn_s_barrier();
@@ -310,6 +365,15 @@ __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
 // Conversion schedule of mlp_bf16.hip: one dword (two values) per unit.
 NL_HD int dword_unit_out(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }
 NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
+constexpr bool same_conversion_schedule() {   // make_train_vm's copies of the two maps
+  for (int m = 0; m < 16; ++m) {
+    if (dword_unit_in(m) != dword_unit_in_c(m)) return false;
+    for (int ku = 1; ku <= 40; ++ku)
+      if (dword_unit_out(ku, m) != dword_unit_out_c(ku, m)) return false;
+  }
+  return true;
+}
+static_assert(same_conversion_schedule(), "the counted seams mirror the conversion schedule");
 // fp16 range contract (NERF_F16X3): an activation at or above 65520 converts to hi = +inf and
 // lo = f16(x - inf) = -inf, so in the next layer every row of that sample's column takes
 // w_hi.inf + w_hi.(-inf) (or 0.inf) = NaN.  One row per column is checked as each layer's
@@ -364,6 +428,7 @@ struct TrainSink {
   unsigned row_w;       // LDS: this lane's sample row in the wave's staging block
   unsigned row_r;       // LDS: the flush's read address (sample lane / 16, piece lane % 16)
   int lane;
+  unsigned mb_off;      // byte offset of the (clamped) sample's ReLU-bit words: one 32-bit VGPR for every store
 };
 __device__ __forceinline__ void lds_store16(unsigned addr, f32x4 v) {
   *(__attribute__((address_space(3))) f32x4*)(uintptr_t)addr = v;
@@ -395,7 +460,10 @@ __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot
       if (pr == 7) {
         const auto sw = __builtin_amdgcn_permlane32_swap(sk.bits[slot], sk.bits[slot], false, false);
 #ifndef NERF_X3_ABLATE_NOSTORE
-        if (sk.valid && h == 0) sk.o.mb[l][sk.p * 8 + t] = unsigned(sw[0]) | unsigned(sw[1]);
+        // counted seams: every lane stores (both halves hold the merged word, and a sample
+        // past the last is clamped to it, the same word) -- no exec branch, one store per tile
+        if (NERF_X3_TRAIN_COUNTED) *(unsigned*)((char*)sk.o.mb[l] + sk.mb_off + 4 * t) = unsigned(sw[0]) | unsigned(sw[1]);
+        else if (sk.valid && h == 0) sk.o.mb[l][sk.p * 8 + t] = unsigned(sw[0]) | unsigned(sw[1]);
 #endif
       }
     }
@@ -424,7 +492,7 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int n = N0 + q * KU + u;
-      seam_before(cx, n);
+      seam_before<kTrain>(cx, n);
       if (u == 0) issue_bias(cx, L, q, acc);
       if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
       wait_lgkm(kTab.u[n].lgkm);
@@ -508,7 +576,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     asm volatile("" : "+s"(cx.blob));   // keep the 132 chunk addresses out of SGPRs across tiles
     const unsigned rows = lds_base + kLdsRowOff + wave_u * kSamplesPerWave * kRowPitch;
     TrainSink sk{tro, p0, p0 < n_points, {0u, 0u}, (tile * kWaves + wave_u) * kSamplesPerWave, n_points,
-                 rows + (lane & 31) * kRowPitch, rows + (lane >> 4) * kRowPitch + (lane & 15) * 16, lane};
+                 rows + (lane & 31) * kRowPitch, rows + (lane >> 4) * kRowPitch + (lane & 15) * 16, lane,
+                 unsigned(p0 < n_points ? p0 : n_points - 1) * 32u};
 #ifdef NERF_X3_ABLATE_PE_ONCE   // timing-only lab build (wrong results): encodings of the first tile reused
     if (tile == blockIdx.x)
 #endif
@@ -541,7 +610,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
         *(u32x4*)(de_dst + 2048 + u * 1024) = lo;
       }
     }
-    wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
+    if (kTrain && NERF_X3_TRAIN_COUNTED) wait_vmcnt(0);   // the seams below count from here
+    else wait_vmcnt(kGldsPerStage * kDmaOutstandingAtSeam);
     __syncthreads();
     if (NERF_X3_REGSTAGE) {
       write_chunk_regs(cx, kStageAhead - 1);
@@ -580,7 +650,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
 #pragma unroll
     for (int i = 0; i < kHeadUnits; ++i) {
       const int n = kHeadUnitBase + i;
-      seam_before(cx, n);
+      seam_before<kTrain>(cx, n);
       if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
       wait_lgkm(4 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf) + seam_writes_since(n));
       __builtin_amdgcn_sched_barrier(0);
