@@ -23,7 +23,7 @@
 // fits in the 512-entry register file of a single wave (accumulators in AGPRs).
 //   * 4 waves x 32 samples = 128 samples per workgroup tile;
 //   * weight units of 4 KiB = the bf16 kernel's 2 KiB unit of W_hi, then W_lo
-//     (nerf_pack_weights_bf16x3 / _f16x3), 4 units per 16 KiB chunk, 3-slot ring;
+//     (nerf_pack_weights_bf16x3 / _f16x3), 4 units per 16 KiB chunk, 3-slot ring (4 in the split-bf16 unit: NERF_X3_SLOTS);
 //   * encodings are the accurate fp32 ones (sincos_acc, as the fp32 path; the training kernels keep ocml sincosf), split
 //     into hi and lo fragments in LDS;
 //   * the ReLU'd fp32 activations are split as they are converted:
@@ -291,14 +291,20 @@ static_assert(!NERF_X3_SPREAD || (kGldsPerStage <= kChunkUnits && kSlots >= 4),
 // body mirror layer_x3 and the heads loop (every store is unconditional: samples past the
 // last are clamped to it); the tile top waits vmcnt(0), so a tile's first two seams count
 // from the tile top.
+#ifndef NERF_X3_ABLATE_NOSTORE
 constexpr int kFlushStores = kSamplesPerWave / 4;        // flush_rows: one 16-B store per 4 lanes' sample
+constexpr int kMaskStores = 1;                           // the tile's ReLU-bit word
+#else   // the timing-only build issues no row or bit stores: the tables must not count them
+constexpr int kFlushStores = 0;
+constexpr int kMaskStores = 0;
+#endif
 struct TrainVm {
   int stores[kUnits];                                    // global stores of unit body n (after its seam)
   int seam[kUnits];                                      // the seam wait before body n, if is_seam(n)
 };
 constexpr void add_sink_stores(TrainVm& t, int n, int l, int tile, int pr) {
   if (pr != 7) return;
-  if (l < 8) t.stores[n] += 1;                           // the tile's ReLU-bit word
+  if (l < 8) t.stores[n] += kMaskStores;                 // the tile's ReLU-bit word
   if (tile & 1) t.stores[n] += kFlushStores;             // the tile pair's rows
 }
 constexpr int dword_unit_out_c(int ku, int m) { return ku >= 16 ? 2 + (m * (ku - 2)) / 16 : m / 4; }

@@ -187,36 +187,49 @@ NL_HD int fp8_k_col(int l, int u, int h, int j) {
   int f = s.extra == kPos ? pe_slot_feature(h, j) : (j < 16 ? dpe_slot_feature(h, j) : -1);
   return f < 0 ? -1 : s.hidden + f;
 }
-// fp8 A blob: 4 KiB units (layer, quarter q, k-step u) = [tile-in-quarter o2][lane 64][32 B],
-// in the bf16 blob's quarter order, zero-padded to a multiple of 8 units (each
-// lane's 32 B split into two 16 B halves p: [o2][p][lane][16 B], so every
-// ds_read_b128 is lane-linear); then the weight scales: per layer [quarter 4]
-// [lane 64][o2 2] u32 whose low byte is the E8M0 scale of row 32*(2q+o2) + (lane&31).
-constexpr int kFp8UnitBytes = 4096;
-NL_HD int fp8_layer_units(int l) { return (out_tiles(l) / 2) * ksteps_fp8(l); }
-NL_HD int fp8_unit_base(int l) {
+// ------------------------------------------------------ fp8, mixed (round 5) --
+// Config 5's network as the fp8 kernel runs it since round 5: L2, L3, L5, L6, L7 and L4's
+// hidden k-steps on the fp8 MFMA; L0, L1, L4's encoding k-steps, C0 and both heads on the
+// bf16 MFMA (v_mfma_f32_32x32x16_bf16); every encoding bf16.  That is the cheapest set of
+// bf16 layers that puts the Lego render at least as close to the reference's fp32 render as
+// the reference's own int8 compressed renderer, in max and mean RGB (tools/fp8_mixed_lab.py,
+// DESIGN.md section 4); the all-fp8 form of rounds 1-4 was 1.9x / 1.2x further off.
+//
+// The stream is 4 KiB units, 4 per 16 KiB chunk, per layer [quarter q][unit], a quarter's
+// fp8 units (k-steps) first, then its bf16 units (two k-steps each), then the head units:
+//   F unit (fp8 k-step u):   [tile-in-quarter o2][half p][lane 64][16 B e4m3]; byte 16p + i of
+//                             lane l is the weight of row 32(2q+o2) + (l&31) at
+//                             fp8_k_col(l, u, l>>5, 16p + i), scaled by the row's 2^-e;
+//   B unit (bf16 k-steps 2b, 2b+1 of the layer's bf16 k-step list): [k-step parity s][o2]
+//                             [lane 64][8 bf16] at bf16_k_col(l, mix_b_kstep(l, b, s), h, j);
+//   H unit (head k-steps 4i..4i+3): [k 4][lane 64][8 bf16] at head_k_row_col (nerf_layout's
+//                             bf16 heads: density over L7's fragments, colour over C0's).
+// Each unit is 128 MFMA cycles either way (2 fp8 MFMAs of 64, or 4 bf16 MFMAs of 32).
+// Then the E8M0 row scales of the fp8 layers: per layer [quarter 4][lane 64][o2 2] u32 whose
+// low byte is the scale of row 32*(2q+o2) + (lane&31) (127 = 1 for the bf16 layers).
+NL_HD bool mix_bf16_layer(int l) { return l == L0 || l == L1 || l == C0; }
+NL_HD int mix_f8_units(int l) { return mix_bf16_layer(l) ? 0 : layer_shape(l).hidden / 64; }
+NL_HD int mix_b_units(int l) {
+  return mix_bf16_layer(l) ? ksteps_bf16(l) / 2 : extra_slots(layer_shape(l).extra) / 16;
+}
+NL_HD int mix_units_per_quarter(int l) { return mix_f8_units(l) + mix_b_units(l); }
+NL_HD int mix_layer_units(int l) { return (out_tiles(l) / 2) * mix_units_per_quarter(l); }
+NL_HD int mix_unit_base(int l) {
   int n = 0;
-  for (int i = 0; i < l; ++i) n += fp8_layer_units(i);
+  for (int i = 0; i < l; ++i) n += mix_layer_units(i);
   return n;
 }
-constexpr int kFp8Units = fp8_unit_base(kNumMfmaLayers);                        // 130
-// Heads of the fp8 path: one 32-row tile accumulated by two kinds of MFMA.
-//   * density (row 3, nerf.py:114): 4 fp8 k-steps over L7's output, i.e. C0's
-//     own hidden B fragments and activation scale.  Two units after C0's, laid
-//     out as fp8 units whose o2 is the k-step's parity: unit i holds k-steps
-//     2i (o2 0) and 2i+1 (o2 1), rows other than 3 zero; the row's E8M0 scale
-//     is the scale table's entry for (layer kNumMfmaLayers, quarter 0, o2 0).
-//   * colour (rows 0-2, nerf.py:123-127): 8 bf16 k-steps (v_mfma_f32_32x32x16_bf16)
-//     over C0's output as bf16 fragments (hid_bf16_feature order), 4 per unit:
-//     [k-step][lane 64][8 bf16] -- the same byte offsets as an fp8 unit's
-//     [o2][p][lane][16 B], so the unit reads as (o2, p) = (k>>1, k&1).
-// fp8 colour was measured 30 % worse in mean RGB error than bf16 colour, fp8
-// density no worse than fp32 density (tests/test_host_layout.py notes).
-constexpr int kFp8DensityUnits = 2, kFp8ColourUnits = 2;
-constexpr int kFp8HeadUnits = kFp8DensityUnits + kFp8ColourUnits;
-constexpr int kFp8UnitsPadded = ((kFp8Units + kFp8HeadUnits + 7) / 8) * 8;      // 136
-constexpr int kFp8ScaleOff = kFp8UnitsPadded * kFp8UnitBytes;                   // bytes
-constexpr int kFp8ScaleBytes = (kNumMfmaLayers + 1) * 4 * 64 * 2 * 4;           // + the heads' row
+// bf16 k-step (bf16_k_col numbering) of element s of B unit b of layer l
+NL_HD int mix_b_kstep(int l, int b, int s) {
+  return (mix_bf16_layer(l) ? 0 : layer_shape(l).hidden / 16) + 2 * b + s;
+}
+constexpr int kFp8UnitBytes = 4096;
+constexpr int kMixLayerUnits = mix_unit_base(kNumMfmaLayers);                  // 162
+constexpr int kMixHeadUnits = kHeadKsteps / 4;                                 // 6
+constexpr int kMixUnits = kMixLayerUnits + kMixHeadUnits;                      // 168
+constexpr int kFp8UnitsPadded = ((kMixUnits + 7) / 8) * 8;                     // 168
+constexpr int kFp8ScaleOff = kFp8UnitsPadded * kFp8UnitBytes;                  // bytes
+constexpr int kFp8ScaleBytes = (kNumMfmaLayers + 1) * 4 * 64 * 2 * 4;
 constexpr int kFp8BlobBytes = kFp8ScaleOff + kFp8ScaleBytes;
 constexpr float kFp8Max = 448.0f;                                              // largest finite e4m3fn
 

@@ -149,58 +149,61 @@ extern "C" int nerf_pack_weights_fp8(const float* const* params, int n_params, u
     if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_fp8: tensor %d is NULL", i);
   auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * kSpecIn[spec] + k]; };
   std::memset(blob, 0, size_t(kFp8BlobBytes));
-  uint8_t* dst = blob;
   uint32_t* scales = reinterpret_cast<uint32_t*>(blob + kFp8ScaleOff);
+  for (int i = 0; i < kFp8ScaleBytes / 4; ++i) scales[i] = 127u;
+  // the mixed stream (nerf_layout.h): per layer [quarter][fp8 units, then bf16 units]
   for (int l = 0; l < kNumMfmaLayers; ++l) {
-    const int spec = kSpecOfLayer[l], nt = out_tiles(l), ku = ksteps_fp8(l), nq = nt / 2;
-    int exps[256];
-    for (int row = 0; row < 32 * nt; ++row) {
-      float m = 0.0f;
-      for (int k = 0; k < kSpecIn[spec]; ++k) m = std::fmax(m, std::fabs(W(spec, row, k)));
-      exps[row] = row_scale_exp(m);
+    const int spec = kSpecOfLayer[l], nt = out_tiles(l), nq = nt / 2, nf = mix_f8_units(l), nb = mix_b_units(l);
+    const int hid = layer_shape(l).hidden;
+    int exps[256] = {};
+    if (nf > 0) {   // row scales over the columns the fp8 k-steps carry (the hidden inputs)
+      for (int row = 0; row < 32 * nt; ++row) {
+        float m = 0.0f;
+        for (int k = 0; k < hid; ++k) m = std::fmax(m, std::fabs(W(spec, row, k)));
+        exps[row] = row_scale_exp(m);
+      }
+      for (int q = 0; q < 4; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int o2 = 0; o2 < 2; ++o2) {
+            const int tile = 2 * q + o2;
+            scales[((l * 4 + q) * 64 + lane) * 2 + o2] = tile < nt ? uint32_t(127 + exps[32 * tile + (lane & 31)]) : 127u;
+          }
     }
-    for (int q = 0; q < 4; ++q)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int o2 = 0; o2 < 2; ++o2) {
-          const int tile = 2 * q + o2;
-          scales[((l * 4 + q) * 64 + lane) * 2 + o2] = tile < nt ? uint32_t(127 + exps[32 * tile + (lane & 31)]) : 127u;
-        }
-    for (int q = 0; q < nq; ++q)
-      for (int u = 0; u < ku; ++u)
+    for (int q = 0; q < nq; ++q) {
+      const int unit0 = mix_unit_base(l) + q * mix_units_per_quarter(l);
+      for (int u = 0; u < nf; ++u) {
+        uint8_t* dst = blob + size_t(unit0 + u) * kFp8UnitBytes;
         for (int o2 = 0; o2 < 2; ++o2)
           for (int p = 0; p < 2; ++p)
             for (int lane = 0; lane < 64; ++lane)
               for (int jj = 0; jj < 16; ++jj) {
-                const int j = 16 * p + jj;
-                const int col = fp8_k_col(l, u, lane >> 5, j);
+                const int col = fp8_k_col(l, u, lane >> 5, 16 * p + jj);
                 const int row = 32 * (2 * q + o2) + (lane & 31);
                 *dst++ = col < 0 ? uint8_t(0) : f32_to_e4m3_rne(std::ldexp(W(spec, row, col), -exps[row]));
               }
+      }
+      for (int b = 0; b < nb; ++b) {
+        uint16_t* dst = reinterpret_cast<uint16_t*>(blob + size_t(unit0 + nf + b) * kFp8UnitBytes);
+        for (int sk = 0; sk < 2; ++sk)
+          for (int o2 = 0; o2 < 2; ++o2)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int j = 0; j < 8; ++j) {
+                const int col = bf16_k_col(l, mix_b_kstep(l, b, sk), lane >> 5, j);
+                const int row = 32 * (2 * q + o2) + (lane & 31);
+                *dst++ = col < 0 ? uint16_t(0) : f32_to_bf16_rne(W(spec, row, col));
+              }
+      }
+    }
   }
-  // the heads (nerf_layout.h kFp8HeadUnits): density row 3 in fp8 over C0's
-  // hidden k-steps, with its own row scale ...
-  float dmax = 0.0f;
-  for (int k = 0; k < kHidden; ++k) dmax = std::fmax(dmax, std::fabs(W(kSpecDensity, 0, k)));
-  const int de = row_scale_exp(dmax);
-  for (int lane = 0; lane < 64; ++lane)
-    for (int o2 = 0; o2 < 2; ++o2)
-      scales[((kNumMfmaLayers * 4) * 64 + lane) * 2 + o2] = (lane & 31) == 3 ? uint32_t(127 + de) : 127u;
-  for (int i = 0; i < kFp8DensityUnits; ++i)
-    for (int o2 = 0; o2 < 2; ++o2)
-      for (int p = 0; p < 2; ++p)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int jj = 0; jj < 16; ++jj) {
-            const int col = fp8_k_col(C0, 2 * i + o2, lane >> 5, 16 * p + jj);
-            *dst++ = (lane & 31) != 3 || col < 0 ? uint8_t(0)
-                                                  : f32_to_e4m3_rne(std::ldexp(W(kSpecDensity, 0, col), -de));
-          }
-  // ... colour rows 0-2 in bf16 over C0's output
-  uint16_t* hd = reinterpret_cast<uint16_t*>(dst);
-  for (int k = 0; k < 4 * kFp8ColourUnits; ++k)
+  // the heads: the bf16 kernel's head tile (nerf_layout.h kHeadKsteps), four k-steps a unit
+  uint16_t* hd = reinterpret_cast<uint16_t*>(blob + size_t(kMixLayerUnits) * kFp8UnitBytes);
+  for (int u = 0; u < kHeadKsteps; ++u)
     for (int lane = 0; lane < 64; ++lane)
       for (int j = 0; j < 8; ++j) {
+        int dens = 0;
         const int row = lane & 31;
-        *hd++ = row < 3 ? f32_to_bf16_rne(W(kSpecColor1, row, hid_bf16_feature(k, lane >> 5, j))) : uint16_t(0);
+        const int f = head_k_row_col(u, row, lane >> 5, j, &dens);
+        *hd++ = f < 0 ? uint16_t(0) : f32_to_bf16_rne(dens ? W(kSpecDensity, 0, f) : W(kSpecColor1, row, f));
       }
   return NERF_OK;
 }

@@ -11,7 +11,7 @@
 // Structure: mlp_x3.h's, run over the backward layers of train_x3_layout.h -- one wave per
 // SIMD, 32 samples per wave, a layer's 8 accumulator tiles issued as 4 quarters, the
 // accumulators of one layer masked, split and kept as the next layer's B fragments, the
-// weight stream through a 3-slot LDS ring filled by LDS-DMA (one barrier per 16 KiB chunk,
+// weight stream through a 4-slot LDS ring (NERF_BWD_X3_SLOTS) filled by LDS-DMA (one barrier per 16 KiB chunk,
 // the stream running on across persistent tiles).  What differs:
 //   * no biases, encodings or heads: the colour-0 layer's inputs are the dZ rows of the
 //     head backward (dhc [P][132]), read at the top of the tile; the density row's term
@@ -83,7 +83,11 @@ NL_HD int dword_unit_in(int m) { return 2 + (m * 10) / 16; }
 // the previous seam: it waits until no more than the ops issued after them -- that interval's
 // mask piece and stores -- are outstanding, and a row store gets a whole chunk to complete
 // instead of stalling the next seam (vmcnt(0) there made the chain wait for HBM writes).
+#ifndef NERF_BWD_X3_ABLATE_NOSTORE
 constexpr int kFlushStores = kSamplesPerWave * 256 / (64 * 16);       // 8 row stores per tile pair
+#else   // the timing-only build stores no rows: the table must count only what is issued
+constexpr int kFlushStores = 0;
+#endif
 struct VmTable {
   int ops[kUnits];      // vector-memory ops unit body n issues after its seam
   int younger[kUnits];  // at the seam of body n: ops issued since the previous seam's stage
@@ -406,6 +410,8 @@ __global__ __launch_bounds__(kThreads, 1) void train_bwd_x3_kernel(const char* _
 
 hipError_t launch_train_bwd_x3(const void* blob, long n_points, const BwdX3Io& io, hipStream_t stream) {
   if (n_points <= 0) return hipSuccess;
+  // request_masks forms a 32-bit byte offset (s * 8 + ...) * 4 into the mask words
+  if (n_points >= (1L << 27)) return hipErrorInvalidValue;
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   hipLaunchKernelGGL(train_bwd_x3_kernel, dim3(unsigned(blocks)), dim3(kThreads), 0, stream, (const char*)blob,

@@ -11,8 +11,9 @@
 // A[row = 32 (2q + o2) + lane % 32][k = 8 (lane / 32) + j] = W_l[hid_bf16_feature(u, lane / 32,
 // j)][row]: the k order the previous backward layer's accumulators give as B fragments.
 // Units are streamed in order in 16 KiB chunks of 4; the colour-0 layer's 8 k-steps make
-// the stream 480 units = 120 chunks, a multiple of the 3-slot ring (the stream runs on
-// across tiles with chunk g always in slot g % 3).
+// the stream 480 units = 120 chunks, a multiple of the 4-slot ring the kernel runs by
+// default (NERF_BWD_X3_SLOTS; 3 slots also divide it), so that the stream runs on across
+// tiles with chunk g always in slot g % slots.
 #pragma once
 #include "nerf_layout.h"
 
@@ -29,7 +30,8 @@ constexpr int kBwdX3Units = bwd_x3_unit_base(kBwdX3Layers);        // 480
 constexpr int kBwdX3UnitBytes = 4096;
 constexpr int kBwdX3ChunkUnits = 4;
 constexpr long kBwdX3BlobBytes = long(kBwdX3Units) * kBwdX3UnitBytes;   // 1.97 MB per net
-static_assert(kBwdX3Units % (3 * kBwdX3ChunkUnits) == 0, "whole chunks, a multiple of the 3-slot ring");
+static_assert(kBwdX3Units % (3 * kBwdX3ChunkUnits) == 0 && kBwdX3Units % (4 * kBwdX3ChunkUnits) == 0,
+              "whole chunks, a multiple of either ring size (3 or 4 slots)");
 // the forward trunk layer whose weights backward layer b >= 1 transposes
 NL_HD int bwd_x3_trunk_layer(int b) { return 8 - b; }
 

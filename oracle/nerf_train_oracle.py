@@ -220,5 +220,5 @@ def step_grads_f64(sd_c, sd_f, image, pose, focal, sel, t_rand, config):
         rgb = volume_render_rgb(s.reshape(n, -1, 1), c.reshape(n, -1, 3), z, rd)
         loss = loss + F.mse_loss(rgb, tgt)
     loss.backward()
-    return float(loss), [{k: v.grad.numpy() for k, v in p.items()} for p in nets]
+    return float(loss.detach()), [{k: v.grad.numpy() for k, v in p.items()} for p in nets]
 

@@ -359,9 +359,87 @@ def main_lego_full(ref_root: str = "/root/reference") -> None:
         json.dump(meta, f, indent=1, sort_keys=True)
 
 
+def main_lego_c3(ref_root: str = "/root/reference") -> None:
+    """BASELINE config 3 (800x600, 64 coarse + 128 importance) on the Lego checkpoint, whole
+    frames, for suite view 0 and the off-axis pose: render_lego_800x600_c3_full.npz.
+
+    The reference's intended chain (src/utils/rendering.py:54-143) with the reference's own
+    pieces wherever one runs: rays and the 64 uniform coarse samples from
+    ``generate_rays`` / ``sample_points_on_rays`` (base_renderer.py:223-281), the COARSE
+    ``NeRFModel`` through ``query_nerf_networks(use_fine=False)`` (:165-188),
+    ``VolumeRenderer.volume_render`` for the weights (rendering.py:102-143); then the oracle's
+    fixed-gather sampler with u = linspace(0, 1, 128) (the reference's ``importance_sample``
+    crashes at its gather, rendering.py:85-90, SURVEY F3 -- build-defined), the sorted union
+    of 192 depths, the FINE ``NeRFModel`` and ``volume_render`` again.  512-ray chunks as
+    ``PyTorchCPURenderer`` (pytorch_renderers.py:137).  Besides RGB and depth, the fixture
+    keeps a 32-bit digest of each ray's 192 fine depths (``oracle.z_row_digest``) so that a GPU
+    test can tell which rays it rendered on the very same samples.  About 6 min a frame on 8
+    cores."""
+    import torch
+
+    sys.path.insert(0, REPO)
+    from oracle import nerf_oracle as O
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    PyTorchCPURenderer, _, _, VolumeRenderer = import_reference(ref_root)
+    coarse_sd, fine_sd = W.lego_models()
+    ckpt_path = os.path.join(tempfile.mkdtemp(prefix="nerf_golden_lego_c3_"), "lego.pth")
+    W.save_checkpoint(ckpt_path, coarse_sd, fine_sd)
+    renderer = PyTorchCPURenderer()
+    renderer.setup(ckpt_path)
+    vr = VolumeRenderer("cpu")
+    poses = suite_poses(2) + [off_axis_pose()]
+    pose_ids = [0, 2]
+    w_, h_, nc, ni = 800, 600, 64, 128
+    out = {"poses": np.stack([poses[i].numpy() for i in pose_ids]), "pose_ids": np.array(pose_ids, dtype=np.int32),
+           "W": np.int32(w_), "H": np.int32(h_), "S_coarse": np.int32(nc), "S_importance": np.int32(ni)}
+    timing = {}
+    for k, pi in enumerate(pose_ids):
+        t0 = time.time()
+        ro, rd = renderer.generate_rays(poses[pi], w_, h_)
+        ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+        rgbs, depths, digests = [], [], []
+        for c in range(0, ro.shape[0], 512):
+            o, d = ro[c:c + 512], rd[c:c + 512]
+            m = o.shape[0]
+            pts, zc = renderer.sample_points_on_rays(o, d, nc)
+            dirs = d[:, None, :].expand(m, nc, 3).reshape(-1, 3)
+            sig, col = renderer.query_nerf_networks(pts.reshape(-1, 3), dirs, use_fine=False)
+            _, _, _, wts = vr.volume_render(sig.reshape(m, nc, 1), col.reshape(m, nc, 3), zc, d)
+            zf = O.fine_z(zc.contiguous(), wts, O.default_u(m, ni))
+            pts = o[..., None, :] + d[..., None, :] * zf[..., :, None]
+            dirs = d[:, None, :].expand(m, nc + ni, 3).reshape(-1, 3)
+            sig, col = renderer.query_nerf_networks(pts.reshape(-1, 3), dirs, use_fine=True)
+            rgb, depth, _, _ = vr.volume_render(sig.reshape(m, -1, 1), col.reshape(m, -1, 3), zf, d)
+            rgbs.append(rgb)
+            depths.append(depth)
+            digests.append(O.z_row_digest(zf))
+            if c % (512 * 100) == 0:
+                print(f"view {pi}: ray {c} of {ro.shape[0]}, {time.time() - t0:.0f} s", flush=True)
+        out[f"rgb_{k}"] = torch.cat(rgbs).reshape(h_, w_, 3).numpy()
+        out[f"depth_{k}"] = torch.cat(depths).reshape(h_, w_).numpy()
+        out[f"zf_digest_{k}"] = np.concatenate(digests).reshape(h_, w_)
+        timing[f"800x600_c3_64+128_view{pi}"] = time.time() - t0
+        print(f"view {pi}: {timing[f'800x600_c3_64+128_view{pi}']:.1f} s", flush=True)
+    np.savez_compressed(os.path.join(HERE, "render_lego_800x600_c3_full.npz"), **out)
+    meta_path = os.path.join(HERE, "golden_lego_meta.json")
+    with open(meta_path) as f:
+        meta = json.load(f)
+    meta.setdefault("render_seconds", {}).update(timing)
+    meta["c3_full_frame"] = {
+        "fine_digest": W.state_dict_digest(fine_sd), "coarse_digest": W.state_dict_digest(coarse_sd),
+        "chain": "reference generate_rays/sample_points_on_rays(64)/coarse NeRFModel/volume_render -> "
+                 "oracle.fine_z (fixed gather, u=linspace(0,1,128), sorted union) -> reference fine NeRFModel/"
+                 "volume_render; build-defined sampler (reference importance_sample crashes, SURVEY F3)"}
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    if "--lego-full" in sys.argv:
+    if "--lego-c3" in sys.argv:
+        main_lego_c3(args[0] if args else "/root/reference")
+    elif "--lego-full" in sys.argv:
         main_lego_full(args[0] if args else "/root/reference")
     elif "--lego" in sys.argv:
         main_lego(args[0] if args else "/root/reference")

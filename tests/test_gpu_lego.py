@@ -256,14 +256,11 @@ def test_lego_headline_full_frames_error_report(ckpt, golden, precision):
 
 
 def test_lego_fp8_vs_reference_compressed(ckpt, golden):
-    """Config 5's error baseline on Lego: fp8 and the reference's own int8 compressed renderer
-    (src/benchmark/compressed_renderer.py, rendered by it: compressed_lego.npz), each against
-    the reference's fp32 render of the same frames (200x150x32, suite view 0 and off-axis).
-    Stated plainly: on this checkpoint fp8 is NOT closer than the int8 renderer in max RGB
-    (CPU emulation, tools/fp8_format_lab.py: e4m3's 4 significant bits in both operands;
-    with bf16 activations and e4m3 weights the max error only reaches the int8 renderer's).
-    The bound catches a broken kernel: within 2.5x of the compressed renderer's max and
-    mean error."""
+    """Config 5's bar on Lego: the fp8 path at least as close to the reference's fp32 render as
+    the reference's own int8 compressed renderer (src/benchmark/compressed_renderer.py, rendered
+    by it: compressed_lego.npz), in max AND mean RGB, on suite view 0 and the off-axis pose
+    (200x150x32).  Round 5's kernel keeps L0, L1, C0, the heads and the encodings on the bf16
+    MFMA (tools/fp8_mixed_lab.py; the all-fp8 network of rounds 1-4 was 1.9x further off in max)."""
     g, gc = golden("render_lego_200x150_s32"), golden("compressed_lego")
     r = renderer(ckpt, "fp8")
     for kc, kg in ((0, 0), (1, 2)):
@@ -275,4 +272,4 @@ def test_lego_fp8_vs_reference_compressed(ckpt, golden):
               f"mean {e8.mean():.3e}; reference int8 compressed rgb max {ec.max():.3e} mean {ec.mean():.3e}; "
               f"fp8 closer in max: {bool(e8.max() < ec.max())}, in mean: {bool(e8.mean() < ec.mean())}")
         assert np.isfinite(e8).all()
-        assert e8.max() < 2.5 * ec.max() and e8.mean() < 2.5 * ec.mean()
+        assert e8.max() < ec.max() and e8.mean() < ec.mean()

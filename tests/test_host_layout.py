@@ -297,59 +297,74 @@ def test_fp8_activation_round_saturates():
     assert np.array_equal(got, [0.0, 0.0, 0.0, 0.0, 2.0 ** -8, 0.3125, 1.0, 448.0, 448.0, 448.0, 448.0, 448.0])
 
 
+FP8_UNITS, FP8_LAYER_UNITS = 168, 162          # nerf_layout.h kMixUnits, kMixLayerUnits
+FP8_BF16 = {0, 1, 8}                           # L0, L1, C0 on the bf16 MFMA (mlp_fp8.hip, round 5)
+
+
+def hid_bf16(u, h, j):
+    return 32 * (u >> 1) + 16 * (u & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+
+
 def emulate_fp8(blob, prm, pe, dpe):
-    """Kernel lane maps of the fp8 path (nerf_layout.h), float64 accumulation."""
+    """Kernel lane maps of the mixed fp8 path (nerf_layout.h "fp8, mixed"), float64
+    accumulation: per layer and quarter the fp8 units ([o2][p][lane][16 B] e4m3, the row's
+    E8M0 scale), then the bf16 units ([s][o2][lane][8 bf16], two k-steps), then the six head
+    units ([k][lane][8 bf16])."""
     n = pe.shape[1]
-    scale_off = 136 * 4096
-    scales = blob[scale_off:].view(np.uint32).reshape(10, 4, 64, 2)
-    off = 0
-    x = xq = None
+    scales = blob[FP8_UNITS * 4096:].view(np.uint32).reshape(10, 4, 64, 2)
+    units = blob[:FP8_UNITS * 4096].reshape(FP8_UNITS, 4096)
+    ext_all = {"pos": [round_bf16(slot_values(pe, h, 32, pe_slot_feature)) for h in range(2)],
+               "dir": [round_bf16(slot_values(dpe, h, 16, dpe_slot_feature)) for h in range(2)]}
+    nu = 0
+    x = x7 = None
     for li, (_, out, hidden, extra) in enumerate(LAYERS):
         nt, nq = out // 32, out // 64
-        ku = hidden // 64 + (1 if extra else 0)
+        bf = li in FP8_BF16
+        n_ext = {"pos": 4, "dir": 2, None: 0}[extra]
+        nf = 0 if bf else hidden // 64
+        nb = (hidden // 16 + n_ext) // 2 if bf else n_ext // 2
+        kh = hidden // 16
         acc = np.tile(unpack_bias(prm, li, nt)[:, None], (1, n))
-        raw = blob[off: off + nq * ku * 4096]
-        off += nq * ku * 4096
-        a = e4m3_decode(raw).reshape(nq, ku, 2, 2, 64, 16)            # [q][u][o2][p][lane][16]
-        a = a.transpose(0, 1, 2, 4, 3, 5).reshape(nq, ku, 2, 64, 32)   # [q][u][o2][lane][byte j]
-        if x is not None:
-            xq = O.fp8_activation_round(x)
-        if extra:
-            feats, fn, used = (pe, pe_slot_feature, 32) if extra == "pos" else (dpe, dpe_slot_feature, 16)
-            ext = [e4m3_round(np.stack([feats[fn(h, j)] if (j < used and fn(h, j) >= 0) else np.zeros(n)
-                                        for j in range(32)])) for h in range(2)]
+        xq = None if x is None else O.fp8_activation_round(x)
+        xb = None if x is None else round_bf16(np.maximum(x, 0))
         for q in range(nq):
-            for o2 in range(2):
-                t = 2 * q + o2
-                for lane in range(64):
-                    r, h = lane & 31, lane >> 5
-                    s = np.ldexp(1.0, int(scales[li, q, lane, o2] & 0xFF) - 127)
-                    row = 32 * t + r
-                    for u in range(ku):
-                        if u < hidden // 64:
-                            b = xq[[32 * (2 * u + (j >> 4)) + acc_row(j & 15, h) for j in range(32)]]
+            for u in range(nf):
+                a = e4m3_decode(units[nu]).reshape(2, 2, 64, 16).transpose(0, 2, 1, 3).reshape(2, 64, 32)
+                nu += 1
+                for o2 in range(2):
+                    for lane in range(64):
+                        r, h = lane & 31, lane >> 5
+                        sc = np.ldexp(1.0, int(scales[li, q, lane, o2] & 0xFF) - 127)
+                        b = xq[[32 * (2 * u + (j >> 4)) + acc_row(j & 15, h) for j in range(32)]]
+                        acc[32 * (2 * q + o2) + r] += sc * (a[o2, lane].astype(np.float64) @ b)
+            for ub in range(nb):
+                a = bf16_to_f32(units[nu].view(np.uint16)).reshape(2, 2, 64, 8)          # [s][o2][lane][j]
+                nu += 1
+                for sk in range(2):
+                    ks = (0 if bf else kh) + 2 * ub + sk
+                    for lane in range(64):
+                        r, h = lane & 31, lane >> 5
+                        if ks < kh:
+                            b = xb[[hid_bf16(ks, h, j) for j in range(8)]]
                         else:
-                            b = ext[h]
-                        acc[row] += s * (a[q, u, o2, lane].astype(np.float64) @ b)
-        x = np.maximum(acc, 0)
-    # heads: density row 3 as 4 fp8 k-steps over C0's quantised input (xq, still
-    # L7's), at the row scale of table entry (9, 0, lane, 0) ...
-    a = e4m3_decode(blob[off: off + 2 * 4096]).reshape(2, 2, 2, 64, 16)
-    a = a.transpose(0, 1, 3, 2, 4).reshape(4, 64, 32)                 # [k-step][lane][byte j]
+                            e = ks - kh
+                            b = ext_all[extra][h][8 * e: 8 * e + 8]
+                        for o2 in range(2):
+                            acc[32 * (2 * q + o2) + r] += a[sk, o2, lane].astype(np.float64) @ b
+        x = acc
+        if li == 7:
+            x7 = acc
+    assert nu == FP8_LAYER_UNITS
+    # heads: one bf16 tile, k-steps 0..15 density over L7's output, 16..23 colour over C0's
+    a = bf16_to_f32(units[FP8_LAYER_UNITS:].view(np.uint16)).reshape(24, 64, 8)          # [k-step][lane][j]
+    x7b, xcb = round_bf16(np.maximum(x7, 0)), round_bf16(np.maximum(x, 0))
     out = np.zeros((4, n))
-    for lane in (3, 35):
-        h = lane >> 5
-        s = np.ldexp(1.0, int(scales[9, 0, lane, 0] & 0xFF) - 127)
-        for u in range(4):
-            b = xq[[32 * (2 * u + (j >> 4)) + acc_row(j & 15, h) for j in range(32)]]
-            out[3] += s * (a[u, lane].astype(np.float64) @ b)
-    # ... colour rows 0-2 as 8 bf16 k-steps over C0's ReLU'd output
-    c = bf16_to_f32(blob[off + 2 * 4096: off + 4 * 4096].view(np.uint16)).reshape(8, 2, 32, 8)   # [k][h][row][j]
-    xr = round_bf16(x)
-    for u in range(8):
-        for h in range(2):
-            for j in range(8):
-                out[:3] += np.outer(c[u, h, :3, j], xr[32 * (u >> 1) + 16 * (u & 1) + 8 * (j >> 2) + 4 * h + (j & 3)])
+    for u in range(24):
+        src, v = (x7b, u) if u < 16 else (xcb, u - 16)
+        for lane in range(64):
+            r, h = lane & 31, lane >> 5
+            if r < 4:
+                out[r] += a[u, lane].astype(np.float64) @ src[[hid_bf16(v, h, j) for j in range(8)]]
     return np.maximum(out[3] + prm[2560], 0), 1 / (1 + np.exp(-(out[:3] + prm[2948:2951, None])))
 
 
@@ -358,7 +373,7 @@ def test_fp8_packing_computes_the_mlp(samples):
     sd = W.synthetic_state_dict(1)
     blob = rt.pack_weights_fp8(sd)
     _, _, prm = rt.pack_weights(sd)
-    assert blob.size == 136 * 4096 + 10 * 4 * 64 * 2 * 4
+    assert blob.size == FP8_UNITS * 4096 + 10 * 4 * 64 * 2 * 4
     s_emu, rgb_emu = emulate_fp8(blob, prm, pe[:, :6], dpe[:, :6])
     s_dir, rgb_dir = O.fp8_mlp_restated(sd, pe[:, :6], dpe[:, :6], chain=False)
     np.testing.assert_allclose(s_emu, s_dir, rtol=1e-6, atol=1e-6)

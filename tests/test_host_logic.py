@@ -379,3 +379,24 @@ def test_plugin_signatures_match_reference():
     assert set(fx["BaseUnifiedRenderer.__init__.attributes"]) <= set(vars(probe))
     for k, v in fx["BaseUnifiedRenderer.__init__.values"].items():
         assert repr(getattr(probe, k)) == v, k
+
+
+def test_bench_self_launch_prints_one_line_world2():
+    """`python bench.py --gpus 2` started plainly (no torchrun environment, as a driver may
+    start it): bench.py launches torch.distributed.run --nproc-per-node 2 as a child process
+    and relays exactly one JSON line, from rank 0, with n_gpus 2 (gloo, no GPU work)."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT", "NERF_BENCH_SELF_LAUNCHED")}
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--launch-check"], capture_output=True, text=True, timeout=180, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["launch_check"] and line["launched_by"] == "self"
+    assert line["steps"] == 3 and line["warmup"] == 1

@@ -1,20 +1,35 @@
-"""Static check of the split training forward's counted seam waits (mlp_x3.h, TrainVm) on
-the emitted listing: walking the tile loop's straight-line body, at every seam (an
-`s_waitcnt vmcnt(N)` followed by `s_barrier`) the chunk the barrier publishes was staged by
-the LDS-DMA group after the barrier two seams back (the tile top counts as one); the wait
-is sound when N <= the vector-memory operations issued after that group's last piece.
+"""Static check of counted seam waits against the emitted listing: the split training
+forward (mlp_x3.h, TrainVm; kernel mlp_x3_kernel<false, true, OpBf16>) and the split
+backward-data chain (train_bwd_x3.hip, kVm; kernel train_bwd_x3_kernel).
 
-    python tools/check_train_seams.py nerf-dbr_amd/csrc/build/asm/mlp_bf16x3.s
+Walking the tile loop's straight-line body, at every seam (an `s_waitcnt vmcnt(N)`
+followed by `s_barrier`) the chunk the barrier publishes was staged by the stage group
+after the barrier `--back` seams earlier (the tile top counts as one: both kernels run a
+4-slot ring, chunk j staged at seam j - 3 and needed at seam j - 1).  A stage group is the
+first `--pieces` LDS-DMA pieces issued after that barrier (other LDS-DMA issued right after
+them -- the backward's mask-word piece -- is younger, as the kernels' tables count it).  The
+wait is sound when N <= the vector-memory operations issued after the group's last piece;
+a table that counted more operations than the compiler emitted fails here.
+
+    python tools/check_train_seams.py LISTING.s [--kernel REGEX] [--pieces N] [--back K]
 """
+import argparse
 import re
 import sys
 
 VMEM = re.compile(r"^\s*(global_|buffer_|scratch_|flat_)")
+KERNELS = {
+    "mlp_bf16x3": r"_ZN4nerf12_GLOBAL__N_113mlp_x3_kernelILb0ELb1E\S*",
+    "train_bwd_x3": r"_ZN4nerf12_GLOBAL__N_119train_bwd_x3_kernel\S*",
+}
 
 
-def main(path):
+def check(path, kernel, pieces=None, back=2, verbose=True):
     lines = open(path).read().split("\n")
-    start = [i for i, l in enumerate(lines) if re.match(r"^_ZN4nerf12_GLOBAL__N_113mlp_x3_kernelILb0ELb1E\S*:", l)][0]
+    starts = [i for i, l in enumerate(lines) if re.match(rf"^{kernel}:", l)]
+    if not starts:
+        raise SystemExit(f"{path}: no kernel matching {kernel}")
+    start = starts[0]
     end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
     body = [l.split(";")[0].strip() for l in lines[start:end]]
     body = [l for l in body if l and not l.startswith(".")]
@@ -39,22 +54,27 @@ def main(path):
         elif e[0] == "barrier":
             seams.append((i, last_wait))
             last_wait = None
-    # the DMA group after each barrier: index of its last piece
+
     def group_end(bi):
-        j, last = bi + 1, None
+        """Index of the last piece of the stage group after barrier bi: the first `pieces`
+        LDS-DMA ops (or, without `pieces`, the first contiguous run of them)."""
+        j, last, n = bi + 1, None, 0
         while j < len(ev) and ev[j][0] != "barrier":
             if ev[j][0] == "vm" and ev[j][1]:
-                last = j
+                last, n = j, n + 1
+                if pieces is not None and n == pieces:
+                    return last
             elif ev[j][0] == "vm" and last is not None:
                 break
             j += 1
-        return last
+        return last if pieces is None else None
+
     bad, checked = 0, 0
-    for k in range(2, len(seams)):
+    for k in range(back, len(seams)):
         bi, n = seams[k]
         if n is None:
             continue
-        g_end = group_end(seams[k - 2][0])
+        g_end = group_end(seams[k - back][0])
         if g_end is None:
             continue
         younger = sum(1 for e in ev[g_end + 1:bi] if e[0] == "vm")
@@ -62,9 +82,26 @@ def main(path):
         if n > younger:
             bad += 1
             print(f"seam {k}: vmcnt({n}) but only {younger} vector-memory ops after the chunk it publishes")
-    print(f"{path}: {checked} counted seams checked, {bad} unsound; {len(seams)} barriers")
+    if verbose:
+        print(f"{path} [{kernel}]: {checked} counted seams checked, {bad} unsound; {len(seams)} barriers")
+    return checked, bad
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("listing")
+    ap.add_argument("--kernel", default=None, help="symbol regex, or one of " + ", ".join(KERNELS))
+    ap.add_argument("--pieces", type=int, default=None, help="LDS-DMA pieces per stage group per wave")
+    ap.add_argument("--back", type=int, default=2, help="seams between a chunk's stage and its publication")
+    ap.add_argument("--min-checked", type=int, default=1, help="fail unless at least this many seams were checked")
+    a = ap.parse_args(argv)
+    kernel = KERNELS.get(a.kernel, a.kernel) if a.kernel else KERNELS["mlp_bf16x3"]
+    checked, bad = check(a.listing, kernel, a.pieces, a.back)
+    if checked < a.min_checked:
+        print(f"only {checked} seams checked (< {a.min_checked}): the listing no longer matches the checker")
+        return 1
     return 1 if bad else 0
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1]))
+    sys.exit(main())
