@@ -253,6 +253,9 @@ __device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
 // output tiles and, for encoding inputs, the B fragment's hi and lo.
 template <class Op, class F = typename Op::frag>
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, F (&ra)[kRing][4], F (&rb)[kRing][2]) {
+#ifdef NERF_X3_ABLATE_NOREAD   // timing-only lab build (wrong results): the ring's first fragments reused
+  if (n >= kRing) return;
+#endif
   const int slot = (n / kChunkUnits) % kSlots;
   const unsigned base = slot < kLoSlots ? cx.ring_addr : cx.ring_hi_addr;
   const int off = (slot < kLoSlots ? slot : slot - kLoSlots) * kChunkB + (n % kChunkUnits) * kUnitB;
@@ -397,7 +400,11 @@ __device__ __forceinline__ void convert_dword(const f32x16& tile, int pr, u32x4&
   return;
 #endif
   unsigned h2, l2;
+#ifdef NERF_X3_ABLATE_NORELU   // timing-only lab build (wrong results): the split without the ReLU
+  Op::split_pair(tile[2 * pr], tile[2 * pr + 1], h2, l2);
+#else
   Op::split_pair(relu(tile[2 * pr]), relu(tile[2 * pr + 1]), h2, l2);
+#endif
   fhi[pr & 3] = h2;
   flo[pr & 3] = l2;
 }

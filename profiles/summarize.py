@@ -70,6 +70,17 @@ def main(src: str, dest: str) -> None:
     bench = open(os.path.join(src, "bench_under_rocprof.json")).read().strip()
     out = {"source": os.path.relpath(dest, os.path.dirname(HERE)), "command": "bench.py " + cmd,
            "bench_under_rocprof": json.loads(bench.splitlines()[-1]), "kernels": stats}
+    # the profiled bench printed the traffic of the PREVIOUS collection (pmc_latest.json as it
+    # stood); the summary carries this collection's own counters in its place and keeps the
+    # printed value beside them, labelled
+    roof = out["bench_under_rocprof"].get("roofline", {})
+    k = roof.get("kernel")
+    if k in stats and "hbm_bytes_per_launch" in stats[k]:
+        roof["traffic_as_printed"] = roof.get("traffic")
+        roof["traffic_as_printed_source"] = roof.get("traffic_source")
+        roof["traffic"] = stats[k]["hbm_bytes_per_launch"]
+        roof["traffic_source"] = (f"this collection's rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `{out['command']}` "
+                                  f"({out['source']}); bytes/launch, FETCH_SIZE x2 (gfx950)")
     json.dump(out, open(os.path.join(dest, "summary.json"), "w"), indent=1)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dest, "kernel_stats.csv"))
     # merge the MLP kernels into pmc_latest.json (one entry per precision's kernel)

@@ -400,3 +400,18 @@ def test_bench_self_launch_prints_one_line_world2():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["launch_check"] and line["launched_by"] == "self"
     assert line["steps"] == 3 and line["warmup"] == 1
+
+
+def test_fp8_mixed_mac_split():
+    """bench.py's ceiling for the mixed fp8 kernel (mlp_fp8.hip, round 5): the MACs it runs on
+    the bf16 MFMA (L0, L1, L4's encoding inputs, C0, both heads) and on the fp8 MFMA (L2, L3,
+    L5-L7, L4's hidden inputs) add up to the network's, from the layer shapes."""
+    import bench
+    from oracle import nerf_oracle as O
+
+    macs = {n: o * i for n, o, i in W.LAYER_SPECS}
+    bf16 = sum(macs[n] for n in O.FP8_BF16_LAYERS) + 256 * W.POS_DIM + macs["density_head"] + macs["color_layers.1"]
+    fp8 = sum(macs[f"layers.{i}"] for i in (2, 3, 5, 6, 7)) + 256 * 256
+    assert bench.FP8_MIX_MACS == {"bf16": bf16, "fp8": fp8}
+    assert bf16 + fp8 == W.MACS_PER_SAMPLE
+    assert abs(bench.FP8_MIX_CEILING - 3983.8) < 0.1
