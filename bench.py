@@ -743,10 +743,13 @@ def cpu_baseline(budget_s):
         for key, (w, h, s) in (("200x150x32", (200, 150, 32)), ("400x300x64", (400, 300, 64)),
                                ("800x600x128", (800, 600, 128))):
             est, _ = rate(w, h, s, 1)
-            rows = int(min(h, max(2, share[key] * budget_s * est / (2 * w))))
-            v, per_view = rate(w, h, s, rows)
+            # two timed repeats of half the budget each; the cell reports the faster (the host is
+            # a shared 16-CPU share of a busy machine: one slow repeat is load, not the renderer)
+            rows = int(min(h, max(2, share[key] * budget_s * est / (4 * w))))
+            reps = [rate(w, h, s, rows) for _ in range(2)]
+            v, per_view = max(reps, key=lambda r: r[0])
             cells[key] = {"rays_per_s": v, "rows": rows, "rays_timed": 2 * rows * w,
-                          "seconds_per_view": per_view}
+                          "seconds_per_view": per_view, "repeats_rays_per_s": [r[0] for r in reps]}
         load1 = loadavg()
     finally:
         torch.set_num_threads(prev)
@@ -754,7 +757,8 @@ def cpu_baseline(budget_s):
     return {"value": head["rays_per_s"], "unit": "rays/s", "cores": threads, "kind": "port",
             "sample": (f"oracle render_image (PyTorch-CPU restatement of PyTorchCPURenderer, 512-ray chunks), "
                        f"2 views of generate_test_poses(2), centre band of {head['rows']} rows of 800x600x128 "
-                       f"per view ({head['rays_timed']} rays), {threads} torch threads, torch {torch.__version__}"),
+                       f"per view ({head['rays_timed']} rays), the faster of 2 repeats, {threads} torch threads, "
+                       f"torch {torch.__version__}"),
             "threads": threads, "host": info, "cells": cells,
             "loadavg_1_5_15min": {"start": load0, "end": load1}}
 

@@ -41,10 +41,14 @@ enum nerf_status {
 enum nerf_precision {
   NERF_FP32 = 0, /* f32-in MFMA (v_mfma_f32_32x32x2_f32); the parity path   */
   NERF_BF16 = 1, /* bf16-in MFMA (v_mfma_f32_32x32x16_bf16), f32 accumulate */
-  NERF_FP8 = 2,  /* e4m3 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4): per-row weight
-                    scales, activations e4m3 at scale 1 saturated at 448, f32 accumulate; the
+  NERF_FP8 = 2,  /* fp8 mixed with bf16 (round 5): L2, L3, L5-L7 and L4's hidden inputs on
+                    the e4m3 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4: per-row weight scales,
+                    activations e4m3 at scale 1 saturated at 448), L0, L1, L4's encoding inputs,
+                    C0, the heads and every encoding on the bf16 MFMA; f32 accumulate.  The
                     compressed-weights path (config 5; the reference's int8
-                    CompressedNeRFRenderer, src/benchmark/compressed_renderer.py) */
+                    CompressedNeRFRenderer, src/benchmark/compressed_renderer.py, is its error
+                    bar: on the Lego checkpoint this path is the closer of the two to the fp32
+                    render, in max and mean RGB) */
   NERF_BF16X3 = 3, /* split bf16 on the bf16 MFMA: W.X ~ Wh.Xh + Wh.Xl + Wl.Xh with
                       v = vh + vl, vh = bf16(v), vl = bf16(v - vh); f32 accumulate,
                       accurate encodings: a parity-grade fast path (RGB/depth

@@ -294,6 +294,26 @@ __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (
     }
 }
 
+// NERF_BF16_SCHED (lab knob): an explicit issue pattern for a unit body's scheduling region
+// (sched_group_barrier): 1: per MFMA 1 MFMA, 1 DS read, 1 VALU; 2: per MFMA 1 MFMA, 2 VALU, 1 DS read.
+#ifndef NERF_BF16_SCHED
+#define NERF_BF16_SCHED 0
+#endif
+__device__ __forceinline__ void sched_unit_pattern() {
+#pragma unroll
+  for (int i = 0; i < 2 * kCols; ++i) {
+    if (NERF_BF16_SCHED == 1) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    } else if (NERF_BF16_SCHED == 2) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  }
+}
+
 template <int L>
 __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[kCols][16], u32x4 (&bout)[kCols][16],
                                            bf16x8 (&ra)[kRing][2], bf16x8 (&rb)[kRing][kCols], const Ctx& cx) {
@@ -339,6 +359,7 @@ __device__ __forceinline__ void layer_bf16(f32x16 (&acc)[kCols][8], u32x4 (&bh)[
           for (int c = 0; c < kCols; ++c)
             convert_dword(acc[c][2 * q - 2 + t], pr, bout[c][2 * (2 * q - 2 + t) + (pr >> 2)]);
       }
+      if (NERF_BF16_SCHED) sched_unit_pattern();
     }
   }
 }

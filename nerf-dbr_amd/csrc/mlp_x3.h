@@ -489,6 +489,35 @@ __device__ __forceinline__ void sink_dword(TrainSink& sk, int l, int t, int slot
   }
 }
 
+// NERF_X3_SCHED (lab knob): an explicit issue pattern for a unit body's scheduling region
+// (sched_group_barrier), so that the region's VALU (conversions) and LDS reads sit between the
+// MFMAs instead of where the compiler's scheduler clumps them (one wave per SIMD hides ~5
+// single-issue instructions per 32-cycle MFMA gap, MI355X_MICROARCH.md constants table).
+//   1: per MFMA: 1 MFMA, 1 DS read, 2 VALU;   2: per MFMA: 1 MFMA, 2 VALU, 1 DS read;
+//   3: per MFMA: 1 MFMA, 1 VALU, 1 DS read, 1 VALU.
+#ifndef NERF_X3_SCHED
+#define NERF_X3_SCHED 0
+#endif
+__device__ __forceinline__ void sched_unit_pattern() {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (NERF_X3_SCHED == 1) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    } else if (NERF_X3_SCHED == 2) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    } else if (NERF_X3_SCHED == 3) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  }
+}
+
 // One layer: reads the previous layer's fragments (ih/il), fills the next's (oh/ol).
 template <int L, bool kTrain, class Op, class F = typename Op::frag>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
@@ -530,6 +559,7 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
           sink_dword<kTrain>(sk, L, 2 * q - 2 + t, t, acc[2 * q - 2 + t], pr, cx.h);
         }
       }
+      if (NERF_X3_SCHED && !kTrain) sched_unit_pattern();
     }
   }
 }
