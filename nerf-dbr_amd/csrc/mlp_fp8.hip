@@ -213,6 +213,16 @@ __device__ __forceinline__ void convert_tile(const f32x16& t, i32x8& b, int off)
   for (int d = 0; d < 4; ++d)
     b[off + d] = cvt4(relu_sat(t[4 * d]), relu_sat(t[4 * d + 1]), relu_sat(t[4 * d + 2]), relu_sat(t[4 * d + 3]));
 }
+// one quarter of that (dword d of the B operand half)
+__device__ __forceinline__ void convert_piece(const f32x16& t, i32x8& b, int off, int d) {
+  b[off + d] = cvt4(relu_sat(t[4 * d]), relu_sat(t[4 * d + 1]), relu_sat(t[4 * d + 2]), relu_sat(t[4 * d + 3]));
+}
+// NERF_FP8_CONV (lab knob): 1 (default) spreads each conversion over the units of its quarter
+// and never converts a tile in the unit right after the MFMA that finished it; 0 converts a whole
+// fp8 tile per unit (units 1, 2) and starts the bf16 conversions at unit 0.
+#ifndef NERF_FP8_CONV
+#define NERF_FP8_CONV 1
+#endif
 // ReLU after rounding, on the packed bf16 words (RNE keeps sign and order): v_cvt_pk_bf16_f32,
 // then v_pk_max_i16 with 0.
 __device__ __forceinline__ unsigned cvt_relu_pair(float lo, float hi) {
@@ -288,27 +298,41 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
       }
       // the previous layer's tiles 6, 7 -> this layer's input, before its unit reads them
       if (q == 0 && in_f8(L)) {
-        if (u == 1) convert_tile(acc[6], b8in[3], 0);
-        if (u == 2) convert_tile(acc[7], b8in[3], 4);
+        if (NERF_FP8_CONV) {   // 8 pieces over units 1, 2 (unit 3 reads them)
+#pragma unroll
+          for (int pc = 0; pc < 8; ++pc)
+            if (1 + pc / 4 == u) convert_piece(acc[6 + (pc >> 2)], b8in[3], 4 * (pc >> 2), pc & 3);
+        } else {
+          if (u == 1) convert_tile(acc[6], b8in[3], 0);
+          if (u == 2) convert_tile(acc[7], b8in[3], 4);
+        }
       }
       if (q == 0 && in_b16(L)) {
 #pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if ((m * 6) / 16 == u) bf16_dword(acc, 6, m, b16);   // k-steps 12..15 are read by unit 6
+        for (int m = 0; m < 16; ++m)   // k-steps 12..15 are read by unit 6
+          if ((NERF_FP8_CONV ? 1 + (m * 5) / 16 : (m * 6) / 16) == u) bf16_dword(acc, 6, m, b16);
       }
       // this layer's final tiles 2q-2, 2q-1 -> the next layer's operand type
       if (q >= 1) {
         if (OUT == kOutF8) {
-          if (u == 1) convert_tile(acc[2 * q - 2], b8out[q >= 1 ? q - 1 : 0], 0);
-          if (u == 2) convert_tile(acc[2 * q - 1], b8out[q >= 1 ? q - 1 : 0], 4);
+          if (NERF_FP8_CONV) {   // 8 pieces over units 1 .. UPQ-1
+#pragma unroll
+            for (int pc = 0; pc < 8; ++pc)
+              if (1 + (pc * (UPQ - 1)) / 8 == u)
+                convert_piece(acc[2 * q - 2 + (pc >> 2)], b8out[q >= 1 ? q - 1 : 0], 4 * (pc >> 2), pc & 3);
+          } else {
+            if (u == 1) convert_tile(acc[2 * q - 2], b8out[q >= 1 ? q - 1 : 0], 0);
+            if (u == 2) convert_tile(acc[2 * q - 1], b8out[q >= 1 ? q - 1 : 0], 4);
+          }
         } else if (OUT == kOutB16) {
 #pragma unroll
           for (int m = 0; m < 16; ++m)
-            if ((m * UPQ) / 16 == u) bf16_dword(acc, 2 * q - 2, m, b16);
+            if ((NERF_FP8_CONV ? (UPQ - 1) - ((15 - m) * (UPQ - 1)) / 16 : (m * UPQ) / 16) == u)
+              bf16_dword(acc, 2 * q - 2, m, b16);
         } else {   // C0's tiles 0, 1 -> colour k-steps 16..19 (its tiles 2, 3 in the head units)
 #pragma unroll
           for (int m = 0; m < 16; ++m)
-            if ((m * UPQ) / 16 == u) bf16_dword(acc, 0, m, hb);
+            if ((NERF_FP8_CONV ? 1 + (m * (UPQ - 1)) / 16 : (m * UPQ) / 16) == u) bf16_dword(acc, 0, m, hb);
         }
       }
     }
