@@ -9,14 +9,15 @@
 // 32-row tile after C0 (nerf_layout.h kHeadUnits): their fp32 VALU form was
 // ~450 instructions per wave, and this kernel's time tracks its VALU count.
 //
-// Geometry: 512-thread workgroups of 256 samples, 8 waves (two per SIMD), each
-// owning one 32-sample column tile.  A lane keeps one layer's 8 accumulator
-// tiles (128 fp32) and the previous layer as packed bf16 B fragments (64
-// VGPRs): activations never leave registers (nerf_layout.h).  The position and
-// direction encodings wait in LDS for the layers that take them.  (-D
-// NERF_BF16_WAVES=4 builds the one-wave-per-SIMD variant: two column tiles per
-// wave; it spills)  Timing ablations and the other lab variants
-// of round 1 are not part of this source.
+// Geometry: workgroups of 256 samples.  The shipped build (round 5, Makefile:
+// NERF_BF16_WAVES=4, VGPR-form, NERF_BF16_SCHED=2) runs 4 waves, one per SIMD, each
+// owning two 32-sample column tiles, so every A fragment read from LDS feeds both
+// columns' MFMAs; a lane keeps both columns' accumulator tiles (VGPRs) and B fragments
+// (AGPRs), 442 registers, no scratch.  The source default (NERF_BF16_WAVES=8) is the
+// rounds 1-4 form: 8 waves, two per SIMD, one column each (128 accumulator + 64
+// fragment VGPRs).  Activations never leave registers (nerf_layout.h); the position and
+// direction encodings wait in LDS for the layers that take them.  Timing ablations and
+// the other lab variants of round 1 are not part of this source.
 //
 // Quarter schedule.  Each layer is issued in quarters of two output tiles.
 // A layer's output tiles are converted to the next layer's bf16 fragments
@@ -295,7 +296,8 @@ __device__ __forceinline__ void issue_bias(const Ctx& cx, int l, int q, f32x16 (
 }
 
 // NERF_BF16_SCHED (lab knob): an explicit issue pattern for a unit body's scheduling region
-// (sched_group_barrier): 1: per MFMA 1 MFMA, 1 DS read, 1 VALU; 2: per MFMA 1 MFMA, 2 VALU, 1 DS read.
+// (sched_group_barrier), per MFMA: 1: 1 MFMA, 1 DS read, 1 VALU; 2: 1 MFMA, 2 VALU, 1 DS read;
+// 3: 1 MFMA, 3 VALU, 1 DS read; 4: 1 MFMA, 1 VALU, 1 DS read, 1 VALU.
 #ifndef NERF_BF16_SCHED
 #define NERF_BF16_SCHED 0
 #endif
@@ -310,6 +312,15 @@ __device__ __forceinline__ void sched_unit_pattern() {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    } else if (NERF_BF16_SCHED == 3) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    } else if (NERF_BF16_SCHED == 4) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     }
   }
 }
