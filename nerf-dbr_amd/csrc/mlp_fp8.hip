@@ -238,6 +238,26 @@ __device__ __forceinline__ void bf16_dword(const f32x16 (&acc)[8], int t, int m,
   f[2 * tile + (pr >> 2)][pr & 3] = cvt_relu_pair(acc[tile][2 * pr], acc[tile][2 * pr + 1]);
 }
 
+// NERF_FP8_SCHED (lab knob): an explicit issue pattern for a unit body's scheduling region
+// (sched_group_barrier), per MFMA: 1: 1 MFMA, 2 VALU, 1 DS read; 2: 1 MFMA, 1 DS read, 3 VALU.
+#ifndef NERF_FP8_SCHED
+#define NERF_FP8_SCHED 0
+#endif
+__device__ __forceinline__ void sched_unit_pattern(int n_mfma) {
+#pragma unroll
+  for (int i = 0; i < n_mfma; ++i) {
+    if (NERF_FP8_SCHED == 1) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    } else if (NERF_FP8_SCHED == 2) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+    }
+  }
+}
+
 // Output conversion of a layer: into the fp8 set, the bf16 set, or C0's colour set.
 enum OutKind { kOutF8 = 0, kOutB16 = 1, kOutColour = 2 };
 NL_HD int out_kind(int l) { return l == C0 ? kOutColour : (l == L0 || l == L7) ? kOutB16 : kOutF8; }
@@ -335,6 +355,7 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
             if ((NERF_FP8_CONV ? 1 + (m * (UPQ - 1)) / 16 : (m * UPQ) / 16) == u) bf16_dword(acc, 0, m, hb);
         }
       }
+      if (NERF_FP8_SCHED) sched_unit_pattern(u < NF ? 2 : 4);
     }
   }
 }
