@@ -69,8 +69,15 @@ def _r(x, fmt):
     return x.to(fmt).to(torch.float32)
 
 
+def mant_cut(v, b):
+    """Round an fp16-valued tensor to b explicit mantissa bits (nearest), as an fp16 bit mask would leave it."""
+    m, e = torch.frexp(v)
+    return torch.ldexp(torch.round(m * 2.0 ** (b + 1)) / 2.0 ** (b + 1), e)
+
+
 def linear(x, w, b, form):
     """x [N, in] fp32, w [out, in], b [out] -> x W^T + b with the form's operand rounding."""
+    b_ = b
     if form == "f32":
         return x @ w.t() + b
     if form.startswith("h"):
@@ -83,6 +90,15 @@ def linear(x, w, b, form):
         else:
             qxh, qxl = block_scaled(x, fmt), block_scaled(xl, fmt)
         return xh @ wh.t() + qxl @ block_scaled(wh, fmt).t() + qxh @ block_scaled(wl, fmt).t() + b
+    if form.startswith("fp16x3t"):   # fp16x3 with the lo parts' mantissas cut to b bits (w: weights, x: activations)
+        which, b = form[7:-1], int(form[-1])
+        xh, wh = _r(x, torch.float16), _r(w, torch.float16)
+        wl, xl = _r(w - wh, torch.float16), _r(x - xh, torch.float16)
+        if "w" in which:
+            wl = mant_cut(wl, b)
+        if "x" in which:
+            xl = mant_cut(xl, b)
+        return xh @ wh.t() + xh @ wl.t() + xl @ wh.t() + b_
     fmt = torch.bfloat16 if form.startswith("bf16") else torch.float16
     xh, wh = _r(x, fmt), _r(w, fmt)
     y = xh @ wh.t()
@@ -144,6 +160,8 @@ def scheme(default, **over):
 
 
 def cost(form):
+    if form.startswith("fp16x3t"):
+        return 3
     return 1 + CROSS_COST[form[1:5]] * 2 if form.startswith("h") else COST[form]
 
 
@@ -165,6 +183,9 @@ SCHEMES = {
     "he2m3": scheme("he2m3"),
     "he3m2": scheme("he3m2"),
 }
+for _b in (2, 3, 4, 6):
+    for _w in ("w", "x", "wx"):
+        SCHEMES[f"fp16x3t{_w}{_b}"] = scheme(f"fp16x3t{_w}{_b}")
 
 
 def main():
