@@ -92,9 +92,10 @@ void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob);
 int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob, uint16_t* bf16_blob,
                       float* param_blob);
 
-/* Pure host helpers for the fp8 path: the packed e4m3 blob (fragments + per-row
- * E8M0 weight scales) the fp8 kernel reads, and the f32 -> e4m3fn (OCP) rounding
- * it uses (round to nearest even; inputs must be within +-448). */
+/* Pure host helpers for the fp8 path: the packed mixed blob the fp8 kernel reads (the fp8
+ * layers' e4m3 fragment units, the bf16 units of L0, L1, C0, L4's encoding inputs and the
+ * heads, then the per-row E8M0 weight scales), and the f32 -> e4m3fn (OCP) rounding it uses
+ * (round to nearest even; inputs must be within +-448). */
 size_t nerf_fp8_blob_bytes(void);
 int nerf_pack_weights_fp8(const float* const* params, int n_params, uint8_t* blob);
 void nerf_f32_to_e4m3(const float* x, int n, uint8_t* out);
