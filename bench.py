@@ -28,6 +28,7 @@ import os
 import sys
 import tempfile
 import time
+from datetime import timedelta
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 for _p in (REPO, os.path.join(REPO, "nerf-dbr_amd")):
@@ -112,10 +113,21 @@ def launch_check(args):
         t = torch.ones(1)
         dist.all_reduce(t)
         world = int(t.item())
+    # the line's host-side fields at this N: the band-scaled traffic and the CPU baseline (run
+    # with the same rank protocol as a real N > 1 bench, at --cpu-seconds)
+    from nerf_amd import distributed as D
+
+    r0, r1 = D.band(rank, world, args.height)
+    kname = {"bf16x3": "mlp_x3_kernel<OpBf16>", "f16x3": "mlp_x3_kernel<OpF16>"}.get(args.precision,
+                                                                                    f"mlp_{args.precision}_kernel")
+    traffic, traffic_src = launch_traffic(kname, args.width, args.height, args.spp, world, (r1 - r0) * args.width)
+    cpu = ranked_cpu_baseline(rank, world, args.cpu_seconds)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "launch_check": True,
-                          "launched_by": "self" if os.environ.get("NERF_BENCH_SELF_LAUNCHED") else "external"}),
+                          "launched_by": "self" if os.environ.get("NERF_BENCH_SELF_LAUNCHED") else "external",
+                          "roofline": {"kernel": kname, "traffic": traffic, "traffic_source": traffic_src},
+                          "cpu_baseline": cpu}),
               flush=True)
     if world > 1:
         dist.barrier()
@@ -351,6 +363,17 @@ FIXTURES = {  # whole frames rendered by the reference (tests/golden/make_golden
     "headline": "render_lego_800x600_s128_full.npz",   # PyTorchCPURenderer.render_image, 800x600x128
     "c3": "render_lego_800x600_c3_full.npz",           # reference pieces + fixed-gather sampler, 64+128
 }
+TRUTH = {"c3": "render_lego_800x600_c3_fp64.npz"}      # the same C3 chain in float64
+
+
+def truth_error(rgb, dep, t_rgb, t_dep):
+    """One frame against the float64 truth: max RGB / depth error, pixels over 1e-4."""
+    import numpy as np
+
+    e_rgb = np.abs(np.asarray(rgb, np.float64) - t_rgb).max(-1)
+    e_dep = np.abs(np.asarray(dep, np.float64) - t_dep)
+    return {"rgb_max_abs": float(e_rgb.max()), "depth_max_abs": float(e_dep.max()),
+            "pixels_over_1e-4": int(((e_rgb >= 1e-4) | (e_dep >= 1e-4)).sum())}
 
 
 def errors_vs_reference(r, which="headline"):
@@ -369,6 +392,10 @@ def errors_vs_reference(r, which="headline"):
     w, h = int(g["W"]), int(g["H"])
     spp = int(g["S"]) if "S" in g else int(g["S_coarse"])
     out = {"reference": os.path.relpath(path, REPO), "views": []}
+    tpath = os.path.join(GOLDEN, TRUTH[which]) if which in TRUTH else None
+    t = np.load(tpath) if tpath and os.path.exists(tpath) else None
+    if t is not None:
+        out["truth"] = os.path.relpath(tpath, REPO)
     for k, pid in enumerate(g["pose_ids"]):
         rgb = torch.full((h, w, 3), float("nan"), device=r.torch_device())
         dep = torch.full((h, w), float("nan"), device=r.torch_device())
@@ -381,12 +408,21 @@ def errors_vs_reference(r, which="headline"):
                              "depth_max_abs": float(e_dep.max()),
                              "pixels_over_1e-4": int(((e_rgb.max(-1) >= 1e-4) | (e_dep >= 1e-4)).sum()),
                              "depth_pixels_gt_1e-2": int((e_dep > 1e-2).sum()), "pixels": int(e_dep.size)})
+        if t is not None:
+            out["views"][-1]["vs_fp64"] = {
+                "this_render": truth_error(rgb.cpu().numpy(), dep.cpu().numpy(), t[f"rgb_{k}"], t[f"depth_{k}"]),
+                "reference_fp32_chain": truth_error(g[f"rgb_{k}"], g[f"depth_{k}"], t[f"rgb_{k}"], t[f"depth_{k}"])}
     v = out["views"]
     out["rgb_max_abs_vs_reference"] = max(x["rgb_max_abs"] for x in v)
     out["rgb_mean_abs_vs_reference"] = float(np.mean([x["rgb_mean_abs"] for x in v]))
     out["depth_max_abs_vs_reference"] = max(x["depth_max_abs"] for x in v)
     out["depth_pixels_gt_1e-2"] = sum(x["depth_pixels_gt_1e-2"] for x in v)
     out["pixels_over_1e-4"] = sum(x["pixels_over_1e-4"] for x in v)
+    if t is not None:
+        out["vs_fp64"] = {who: {"pixels_over_1e-4": sum(x["vs_fp64"][who]["pixels_over_1e-4"] for x in v),
+                                "rgb_max_abs": max(x["vs_fp64"][who]["rgb_max_abs"] for x in v),
+                                "depth_max_abs": max(x["vs_fp64"][who]["depth_max_abs"] for x in v)}
+                          for who in ("this_render", "reference_fp32_chain")}
     return out
 
 
@@ -448,6 +484,25 @@ def other_configs(ckpt, poses, local, ref32):
         "rgb_mean_abs_vs_reference": errh.get("rgb_mean_abs_vs_reference"),
         "depth_pixels_gt_1e-2": errh.get("depth_pixels_gt_1e-2"), "error_vs_reference": errh}
 
+    # C3 on the fp32 path: the reference's arithmetic, its error against the reference's fp32
+    # chain and both against the float64 truth (tests/test_gpu_lego_c3.py (iv))
+    h32 = MI355XRenderer("fp32", n_importance=128, device_index=local)
+    h32.setup(ckpt)
+    h32.hip.set_profiling(True)
+    step, _ = frame_step(h32, poses, 800, 600, 64, 0, 1)
+    dt = time_steps(step, 1, 1, 1) / nv
+    st = h32.hip.stage_ms()
+    mlp_ms = st["coarse_mlp"] + st["fine_mlp"]
+    errh32 = errors_vs_reference(h32, "c3")
+    out["c3_hierarchical_fp32_800x600_64+128"] = {
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms_last_view": st,
+        "mlp_tflops_last_view": flop / (mlp_ms * 1e-3) / 1e12,
+        "mlp_frac_f32_peak_last_view": flop / (mlp_ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"],
+        "rgb_max_abs_vs_reference": errh32.get("rgb_max_abs_vs_reference"),
+        "pixels_over_1e-4": errh32.get("pixels_over_1e-4"), "vs_fp64": errh32.get("vs_fp64"),
+        "depth_pixels_gt_1e-2": errh32.get("depth_pixels_gt_1e-2"), "error_vs_reference": errh32}
+    del h32
+
     # C3 on the gate-passing path (split fp16 for both nets; the hierarchical chain is
     # checked at the 1e-4 gate on Lego in tests/test_gpu_lego.py)
     h3 = MI355XRenderer("f16x3", n_importance=128, device_index=local)
@@ -464,7 +519,7 @@ def other_configs(ckpt, poses, local, ref32):
         "mlp_tflops_last_view": flop / (mlp_ms * 1e-3) / 1e12,
         "mlp_frac_x3_ceiling_last_view": flop / (mlp_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f16x3"],
         "rgb_max_abs_vs_reference": errh3.get("rgb_max_abs_vs_reference"),
-        "pixels_over_1e-4": errh3.get("pixels_over_1e-4"),
+        "pixels_over_1e-4": errh3.get("pixels_over_1e-4"), "vs_fp64": errh3.get("vs_fp64"),
         "depth_pixels_gt_1e-2": errh3.get("depth_pixels_gt_1e-2"), "error_vs_reference": errh3}
     del h3
 
@@ -660,6 +715,51 @@ def training_leg(local, rank, world, n_steps, cpu_seconds):
 
 
 # ------------------------------------------------------------- CPU baseline --
+def launch_traffic(kname, width, height, spp, world, band_rays):
+    """HBM bytes per launch of kernel ``kname`` from profiles/pmc_latest.json (the headline
+    launch's rocprofv3 FETCH_SIZE / WRITE_SIZE passes, collected at N = 1).  At N > 1 the
+    N = 1 figure scaled by this rank's band, labelled as such: the traffic
+    is per sample (segment records, rays, outputs), the 1 MB of weights aside."""
+    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if not os.path.exists(pmc) or (width, height, spp) != (800, 600, 128):
+        return None, None
+    k = json.load(open(pmc)).get("kernels", {}).get(kname, {})
+    if "hbm_bytes_per_launch" not in k:
+        return None, None
+    if world == 1:
+        # profiles/collect.sh profiles the headline bench alone, so every dispatch of this
+        # kernel there is this launch
+        return k["hbm_bytes_per_launch"], (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `{k['command']}` "
+                                           f"({k['source']}); bytes/launch, FETCH_SIZE x2 (gfx950)")
+    return (k["hbm_bytes_per_launch"] * band_rays / (width * height),
+            f"scaled from the N=1 counters (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of `{k['command']}`, "
+            f"{k['source']}) by rank 0's band: {band_rays} of {width * height} rays; not measured at N={world}")
+
+
+def ranked_cpu_baseline(rank, world, budget_s):
+    """The CPU baseline on rank 0.  At N > 1 the same protocol at half the
+    budget, after every rank's GPU work, while the other ranks block in a TCPStore wait (a
+    socket read, no spinning collective) so that the host cores are free."""
+    import torch.distributed as dist
+
+    if budget_s <= 0:
+        return None
+    if world == 1:
+        return cpu_baseline(budget_s)
+    store = dist.distributed_c10d._get_default_store()
+    cpu = None
+    if rank == 0:
+        try:
+            cpu = cpu_baseline(budget_s / 2)
+            cpu["n_gpus_protocol"] = (f"rank 0 of {world}, after the GPU legs, the other ranks idle in a "
+                                      f"TCPStore wait; budget {budget_s / 2:.0f} s (half the N=1 budget)")
+        finally:
+            store.set("nerf_bench_cpu_baseline_done", "1")
+    else:
+        store.wait(["nerf_bench_cpu_baseline_done"], timedelta(seconds=1800))
+    return cpu
+
+
 def host_cpu_info():
     """CPU model; logical CPUs of the machine and of this process's affinity mask;
     physical cores behind that mask; the cgroup CPU quota, if any."""
@@ -834,20 +934,16 @@ def main():
         view_ms.append(1e3 * time_steps(vstep, 1, max(2, args.steps // 2), world))
 
     flop_launch = band_rays * spp * W.FLOPS_PER_SAMPLE
-    traffic, traffic_src = None, None
     kname = {"bf16x3": "mlp_x3_kernel<OpBf16>", "f16x3": "mlp_x3_kernel<OpF16>"}.get(args.precision,
                                                                                     f"mlp_{args.precision}_kernel")
-    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc) and (width, height, spp, world) == (800, 600, 128, 1):
-        # the headline launch's own counters: profiles/collect.sh profiles the
-        # headline bench alone, so every dispatch of this kernel there is this launch
-        k = json.load(open(pmc)).get("kernels", {}).get(kname, {})
-        if "hbm_bytes_per_launch" in k:
-            traffic = k["hbm_bytes_per_launch"]
-            traffic_src = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `{k['command']}` "
-                           f"({k['source']}); bytes/launch, FETCH_SIZE x2 (gfx950)")
+    traffic, traffic_src = launch_traffic(kname, width, height, spp, world, band_rays)
     achieved = flop_launch / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
+    peak_kind = {"bf16": "bf16 dense MFMA peak", "fp32": "f32 MFMA peak",
+                 "bf16x3": "bf16 dense peak / 3 (three MFMAs per product)",
+                 "f16x3": "f16 dense peak / 3 (three MFMAs per product)",
+                 "fp8": (f"mixed fp8/bf16 ceiling of this layer split ({FP8_MIX_CEILING:.0f} TFLOP/s), "
+                         "not the 5000 TFLOP/s fp8 hardware peak")}[args.precision]
 
     extra = {"gpu_clock_timed_region": clocks.summary(),
              "protocol": {"views": "generate_test_poses(2) (benchmark_suite.py:132-149, 188-220)",
@@ -908,9 +1004,7 @@ def main():
     if not args.no_train and not (world > 1 and args.no_extras):
         extra["training"] = training_leg(local, rank, world, args.train_steps, min(10.0, args.cpu_seconds / 3))
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args.cpu_seconds)
+    cpu = ranked_cpu_baseline(rank, world, args.cpu_seconds)
 
     if rank == 0:
         out = {
@@ -937,7 +1031,9 @@ def main():
                                        f"{'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
                                        f"gather to rank 0" if world > 1 else "1 GPU")},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
+                         "frac": achieved / peak, "peak_kind": peak_kind,
+                         **({"frac_fp8_hw_peak": achieved / 5000.0} if args.precision == "fp8" else {}),
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_ms,
                          "flop_per_launch": flop_launch},
             "cpu_baseline": cpu,

@@ -435,9 +435,106 @@ def main_lego_c3(ref_root: str = "/root/reference") -> None:
         json.dump(meta, f, indent=1, sort_keys=True)
 
 
+def _fine_z_f64(z, weights, u):
+    """The oracle's fixed-gather sampler (oracle.importance_sample / fine_z, after
+    rendering.py:72-95) with the dtype of its inputs kept: the float64 truth's sampler."""
+    import torch
+
+    n = z.shape[-1]
+    w = weights + 1e-5
+    pdf = w / torch.cumsum(w, -1)[..., -1:]
+    cdf = torch.cat([torch.zeros_like(pdf[..., :1]), torch.cumsum(pdf, -1)], -1)
+    idx = torch.searchsorted(cdf.contiguous(), u.contiguous(), right=True)
+    below, above = torch.clamp(idx - 1, 0, n - 1), torch.clamp(idx, 0, n - 1)
+    cdf_b, cdf_a = torch.gather(cdf, -1, below), torch.gather(cdf, -1, above)
+    z_b, z_a = torch.gather(z, -1, below), torch.gather(z, -1, above)
+    denom = cdf_a - cdf_b
+    denom = torch.where(denom < 1e-5, torch.ones_like(denom), denom)
+    z_imp = z_b + (u - cdf_b) / denom * (z_a - z_b)
+    return torch.sort(torch.cat([z, z_imp], -1), -1).values
+
+
+def main_lego_c3_fp64(ref_root: str = "/root/reference") -> None:
+    """The float64 truth of BASELINE config 3: the same chain as
+    ``main_lego_c3`` -- the reference's ``generate_rays`` / ``sample_points_on_rays``
+    (base_renderer.py:223-281), its coarse and fine ``NeRFModel`` (nerf.py:92-131) and
+    ``VolumeRenderer.volume_render`` (rendering.py:102-143) with the fixed-gather sampler in
+    between -- run with every tensor in float64 (torch's default dtype set to float64, the
+    models ``NeRFModel()`` built in float64 and loaded with the fp32 checkpoint's values, the
+    pose cast up), for suite view 0 and the off-axis pose: render_lego_800x600_c3_fp64.npz.
+    The fp32 fixture (render_lego_800x600_c3_full.npz) and the GPU renders are both measured
+    against it in tests/test_gpu_lego_c3.py.  About 25 min a frame on 8 cores."""
+    import torch
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    PyTorchCPURenderer, NeRFModel, _, VolumeRenderer = import_reference(ref_root)
+    coarse_sd, fine_sd = W.lego_models()
+    ckpt_path = os.path.join(tempfile.mkdtemp(prefix="nerf_golden_lego_c3_fp64_"), "lego.pth")
+    W.save_checkpoint(ckpt_path, coarse_sd, fine_sd)
+    renderer = PyTorchCPURenderer()
+    renderer.setup(ckpt_path)
+    poses = suite_poses(2) + [off_axis_pose()]
+    torch.set_default_dtype(torch.float64)
+
+    def net(sd):
+        m = NeRFModel()
+        m.load_state_dict({k: torch.from_numpy(v.astype(np.float64)) for k, v in sd.items()})
+        assert all(p.dtype == torch.float64 for p in m.parameters())
+        return m.eval()
+
+    coarse, fine = net(coarse_sd), net(fine_sd)
+    vr = VolumeRenderer("cpu")
+    pose_ids = [0, 2]
+    w_, h_, nc, ni, chunk = 800, 600, 64, 128, 4096
+    out = {"poses": np.stack([poses[i].numpy() for i in pose_ids]), "pose_ids": np.array(pose_ids, dtype=np.int32),
+           "W": np.int32(w_), "H": np.int32(h_), "S_coarse": np.int32(nc), "S_importance": np.int32(ni)}
+    timing = {}
+    with torch.no_grad():
+        for k, pi in enumerate(pose_ids):
+            t0 = time.time()
+            ro, rd = renderer.generate_rays(poses[pi].double(), w_, h_)
+            assert ro.dtype == torch.float64 and rd.dtype == torch.float64
+            ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+            rgbs, depths = [], []
+            for c in range(0, ro.shape[0], chunk):
+                o, d = ro[c:c + chunk], rd[c:c + chunk]
+                m = o.shape[0]
+                pts, zc = renderer.sample_points_on_rays(o, d, nc)
+                sig, col = coarse(pts.reshape(-1, 3), d[:, None, :].expand(m, nc, 3).reshape(-1, 3))
+                _, _, _, wts = vr.volume_render(sig.reshape(m, nc, 1), col.reshape(m, nc, 3), zc, d)
+                u = torch.linspace(0.0, 1.0, ni).expand(m, ni)
+                zf = _fine_z_f64(zc.contiguous(), wts, u)
+                pts = o[..., None, :] + d[..., None, :] * zf[..., :, None]
+                sig, col = fine(pts.reshape(-1, 3), d[:, None, :].expand(m, nc + ni, 3).reshape(-1, 3))
+                rgb, depth, _, _ = vr.volume_render(sig.reshape(m, -1, 1), col.reshape(m, -1, 3), zf, d)
+                assert rgb.dtype == torch.float64
+                rgbs.append(rgb)
+                depths.append(depth)
+                if c % (chunk * 20) == 0:
+                    print(f"view {pi}: ray {c} of {ro.shape[0]}, {time.time() - t0:.0f} s", flush=True)
+            out[f"rgb_{k}"] = torch.cat(rgbs).reshape(h_, w_, 3).numpy()
+            out[f"depth_{k}"] = torch.cat(depths).reshape(h_, w_).numpy()
+            timing[f"800x600_c3_64+128_fp64_view{pi}"] = time.time() - t0
+            print(f"view {pi}: {timing[f'800x600_c3_64+128_fp64_view{pi}']:.1f} s", flush=True)
+    torch.set_default_dtype(torch.float32)
+    np.savez_compressed(os.path.join(HERE, "render_lego_800x600_c3_fp64.npz"), **out)
+    meta_path = os.path.join(HERE, "golden_lego_meta.json")
+    with open(meta_path) as f:
+        meta = json.load(f)
+    meta.setdefault("render_seconds", {}).update(timing)
+    meta["c3_full_frame_fp64"] = {
+        "fine_digest": W.state_dict_digest(fine_sd), "coarse_digest": W.state_dict_digest(coarse_sd),
+        "chain": "the c3_full_frame chain with torch's default dtype float64: reference generate_rays/"
+                 "sample_points_on_rays/NeRFModel (float64 parameters)/volume_render, float64 fixed-gather sampler"}
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    if "--lego-c3" in sys.argv:
+    if "--lego-c3-fp64" in sys.argv:
+        main_lego_c3_fp64(args[0] if args else "/root/reference")
+    elif "--lego-c3" in sys.argv:
         main_lego_c3(args[0] if args else "/root/reference")
     elif "--lego-full" in sys.argv:
         main_lego_full(args[0] if args else "/root/reference")

@@ -19,7 +19,14 @@ tell which rays the GPU rendered on the very samples the reference chain used.
         reference's CPU GEMM summation order) moved by the sampler.  Each such ray is listed
         with the sampler step that moved it (a ``denom < 1e-5`` switch, rendering.py:93, or an
         interpolation t = (u - cdf) / denom in a low-probability bin);
-  (iii) bf16 and fp8 report max / mean RGB and the pixels whose depth moves by > 1e-2.
+  (iii) bf16 and fp8 report max / mean RGB and the pixels whose depth moves by > 1e-2,
+        bounded at 1.5x their round-5 measurement;
+  (iv)  the truth: the same chain in float64 (render_lego_800x600_c3_fp64.npz,
+        ``make_golden.py --lego-c3-fp64``).  The hierarchical chain is ill-conditioned at a few
+        hundred rays per frame (a last-bit change of a coarse weight moves a fine sample), so
+        no fp32 implementation can match another one there; what is asserted is that the GPU's
+        fp32 and f16x3 renders are no further from the float64 truth than the reference's own
+        fp32 chain is -- in pixels over 1e-4 and in max RGB / depth error.
 """
 import os
 
@@ -33,8 +40,9 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
 C3 = "render_lego_800x600_c3_full"
+C3_FP64 = "render_lego_800x600_c3_fp64"
 NC, NI = 64, 128
-MAX_EXPLAINED = 4096            # rays over the gate the oracle re-renders (all of them below this)
+MAX_DW = 1e-5                   # coarse weights GPU vs the oracle's CPU pass on the over-gate rays
 _R = {}
 
 
@@ -103,7 +111,6 @@ def test_lego_c3_full_frames_vs_reference(ckpt, golden, precision):
         bad = np.flatnonzero(over)
         if bad.size == 0:
             continue
-        assert bad.size <= MAX_EXPLAINED, f"{bad.size} pixels outside the gate"
         # the oracle's fine pass on the GPU's own fine samples, for every pixel over the gate
         sel = torch.from_numpy(bad)
         ob, db, zb = o[sel], d[sel], zf[sel]
@@ -138,13 +145,53 @@ def test_lego_c3_full_frames_vs_reference(ckpt, golden, precision):
             print(f"    pixel ({i // w}, {i % w}): rgb err {e_rgb[i]:.2e} depth err {e_dep[i]:.2e}; switch "
                   f"{bool(switch[j])} bin {bool(bin_moved[j])} min denom {min_denom[j]:.2e}")
         assert f_rgb < TOL and f_dep < TOL, "the fine pass on the GPU's own samples is outside the gate"
+        assert dw < MAX_DW, "the coarse weights differ by more than last bits"
         assert not same[bad].any()
 
 
-@pytest.mark.parametrize("precision,max_mean", [("bf16", 2e-2), ("fp8", 6e-2)])
-def test_lego_c3_full_frames_error_report(ckpt, golden, precision, max_mean):
-    """(iii) the throughput paths on the same whole C3 frames: reported; the bounds only catch a
-    broken kernel."""
+def truth_stats(rgb, depth, t_rgb, t_dep):
+    """Error of one frame against the float64 truth: max / mean RGB, max depth, and the pixels
+    whose RGB (any channel) or depth is off by 1e-4 or more."""
+    e_rgb = np.abs(np.asarray(rgb, np.float64).reshape(-1, 3) - t_rgb.reshape(-1, 3)).max(-1)
+    e_dep = np.abs(np.asarray(depth, np.float64).reshape(-1) - t_dep.reshape(-1))
+    return {"rgb_max": float(e_rgb.max()), "rgb_mean": float(e_rgb.mean()), "depth_max": float(e_dep.max()),
+            "over": int(((e_rgb >= TOL) | (e_dep >= TOL)).sum())}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
+def test_lego_c3_no_further_from_fp64_than_reference(ckpt, golden, precision):
+    """(iv) against the float64 run of the same chain (rendering.py:72-143 with the gather fixed,
+    base_renderer.py:165-281, nerf.py:92-131 in float64): the GPU render has no more pixels over
+    1e-4 and no larger max RGB or depth error than the reference's own fp32 chain
+    (render_lego_800x600_c3_full.npz) on the same frames."""
+    g, t = golden(C3), golden(C3_FP64)
+    w, h = int(g["W"]), int(g["H"])
+    r = renderer(ckpt, precision)
+    for k in range(len(g["pose_ids"])):
+        assert np.array_equal(g["poses"][k], t["poses"][k])
+        rgb, depth = r.render_image(torch.from_numpy(g["poses"][k]), (w, h), NC)
+        ref = truth_stats(g[f"rgb_{k}"], g[f"depth_{k}"], t[f"rgb_{k}"], t[f"depth_{k}"])
+        gpu = truth_stats(rgb.cpu().numpy(), depth.cpu().numpy(), t[f"rgb_{k}"], t[f"depth_{k}"])
+        print(f"lego C3 view {int(g['pose_ids'][k])} vs float64: reference fp32 chain rgb max {ref['rgb_max']:.3e} "
+              f"mean {ref['rgb_mean']:.3e} depth max {ref['depth_max']:.3e} over {TOL}: {ref['over']}; GPU {precision} "
+              f"rgb max {gpu['rgb_max']:.3e} mean {gpu['rgb_mean']:.3e} depth max {gpu['depth_max']:.3e} over: {gpu['over']}")
+        assert gpu["over"] <= ref["over"]
+        assert gpu["rgb_max"] <= ref["rgb_max"] and gpu["depth_max"] <= ref["depth_max"]
+
+
+# Per view (suite 0, off-axis): RGB max, RGB mean and pixels with depth moved by > 1e-2 against
+# the fp32 fixture, measured on the driver's round-5 GPU suite (profiles/round5/r5u/gpu_suite.log);
+# bounded at 1.5x (+16 on the count; RGB max only where 1.5x stays below 1).
+C3_MEASURED = {
+    "bf16": [(4.858e-01, 1.153e-03, 20432), (6.551e-01, 6.226e-04, 12441)],
+    "fp8": [(5.155e-01, 4.539e-03, 66700), (9.073e-01, 3.428e-03, 71941)],
+}
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_lego_c3_full_frames_error_report(ckpt, golden, precision):
+    """(iii) the throughput paths on the same whole C3 frames, bounded at 1.5x their round-5
+    measurement per view so that a regression fails."""
     g = golden(C3)
     w, h = int(g["W"]), int(g["H"])
     r = renderer(ckpt, precision)
@@ -153,6 +200,11 @@ def test_lego_c3_full_frames_error_report(ckpt, golden, precision, max_mean):
         e_rgb = np.abs(rgb.cpu().numpy() - g[f"rgb_{k}"])
         e_dep = np.abs(depth.cpu().numpy() - g[f"depth_{k}"])
         n_flip = int((e_dep > 1e-2).sum())
+        m, a, n = C3_MEASURED[precision][k]
+        b_max, b_mean, b_flip = 1.5 * m, 1.5 * a, int(1.5 * n) + 16
         print(f"lego C3 {precision} view {int(g['pose_ids'][k])}: rgb max {e_rgb.max():.3e} mean {e_rgb.mean():.3e}; "
-              f"depth max {e_dep.max():.3e}, pixels with depth error > 1e-2: {n_flip} of {e_dep.size}")
-        assert np.isfinite(e_rgb).all() and e_rgb.mean() < max_mean and n_flip < e_dep.size // 3
+              f"depth max {e_dep.max():.3e}, pixels with depth error > 1e-2: {n_flip} of {e_dep.size} "
+              f"(bounds {min(b_max, 1.0):.3e} / {b_mean:.3e} / {b_flip})")
+        assert np.isfinite(e_rgb).all() and e_rgb.mean() < b_mean and n_flip <= b_flip
+        if b_max < 1.0:
+            assert e_rgb.max() < b_max

@@ -393,13 +393,41 @@ def test_bench_self_launch_prints_one_line_world2():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                            "MASTER_PORT", "NERF_BENCH_SELF_LAUNCHED")}
     p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-                        "--launch-check"], capture_output=True, text=True, timeout=180, env=env, cwd=repo)
+                        "--launch-check", "--cpu-seconds", "0"], capture_output=True, text=True, timeout=180, env=env,
+                       cwd=repo)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, p.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["launch_check"] and line["launched_by"] == "self"
     assert line["steps"] == 3 and line["warmup"] == 1
+
+
+def test_bench_world2_line_carries_cpu_baseline_and_traffic():
+    """at N = 2 (gloo, torchrun, no GPU work) rank 0's line carries a
+    cpu_baseline, run while rank 1 waits on the TCPStore, and the band-scaled roofline traffic,
+    labelled as scaled from the N = 1 counters (half the frame's rays on rank 0's band)."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT", "NERF_BENCH_SELF_LAUNCHED")}
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--cpu-seconds", "2"], capture_output=True, text=True, timeout=300, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    cpu = line["cpu_baseline"]
+    assert cpu["unit"] == "rays/s" and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
+    assert "rank 0 of 2" in cpu["n_gpus_protocol"]
+    pmc = json.load(open(os.path.join(repo, "profiles", "pmc_latest.json")))["kernels"]["mlp_bf16_kernel"]
+    roof = line["roofline"]
+    assert roof["kernel"] == "mlp_bf16_kernel"
+    assert abs(roof["traffic"] - pmc["hbm_bytes_per_launch"] / 2) < 1e-6 * pmc["hbm_bytes_per_launch"]
+    assert "scaled from the N=1 counters" in roof["traffic_source"]
 
 
 def test_fp8_mixed_mac_split():
