@@ -50,9 +50,18 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 static_assert(!NERF_ASM_LDS_READS, "the mixed fp8 kernel reads LDS with compiler-counted loads only");
 
-constexpr int kWaves = 8;
+// NERF_FP8_WAVES: 8 (rounds 1-5) -- two waves per SIMD, one 32-sample column each, waves 4-7
+// one chunk behind (the wave lag below); 4 (round 6) -- one wave per SIMD owning two columns,
+// so every A fragment read from LDS feeds both columns' MFMAs (the bf16 headline's form)
+#ifndef NERF_FP8_WAVES
+#define NERF_FP8_WAVES 8
+#endif
+constexpr int kWaves = NERF_FP8_WAVES;
+constexpr int kCols = 8 / kWaves;                                    // column tiles per wave
+static_assert(kCols == 1 || kCols == 2, "4 or 8 waves");
+constexpr bool kLag = kWaves == 8;                                   // a lagging half of the waves
 constexpr int kThreads = 64 * kWaves;
-constexpr int kSamplesPerBlock = kWaves * kSamplesPerWave;           // 256
+constexpr int kSamplesPerBlock = kWaves * kCols * kSamplesPerWave;   // 256
 constexpr int kUnitB = kFp8UnitBytes;                                // 4 KiB
 constexpr int kUnits = kMixUnits;                                    // 168
 constexpr int kChunkUnits = 4;                                       // 4 KiB units per LDS chunk (one barrier per chunk)
@@ -76,7 +85,19 @@ constexpr int kSlots = 4;
 // of rotation 0 (the ring sits 2 slots above the LDS base, so ring_hi stays a valid
 // address), and a stage's LDS slot is a scalar (c + rot) & 3.
 constexpr int kGldsPerStage = kChunkB / (kThreads * 16);
-constexpr int kPf = 1;                                               // fragment prefetch distance (units)
+// NERF_FP8_AHEAD (4 waves only): a seam stages the chunk 1 (default) or 2 ahead of the one it
+// publishes; with 2, the seam waits for its chunk with the next one still in flight.  The
+// 4-slot ring has room: at seam c every wave's reads of chunk c - 2 have completed (its MFMAs
+// consumed them before the wave reached the seam), so chunk c + 2 takes that slot.
+#ifndef NERF_FP8_AHEAD
+#define NERF_FP8_AHEAD 1
+#endif
+constexpr int kAhead = NERF_FP8_AHEAD;
+static_assert(kAhead == 1 || (kAhead == 2 && !kLag), "two chunks ahead: the one-wave-per-SIMD form");
+#ifndef NERF_FP8_PF
+#define NERF_FP8_PF 1
+#endif
+constexpr int kPf = NERF_FP8_PF;                                     // fragment prefetch distance (units)
 constexpr int kRing = kPf + 1;
 static_assert(kUnits % kChunkUnits == 0 && kUnits % kRing == 0, "the next tile's unit n uses ring entry n % kRing");
 static_assert(kTotalChunks % 2 == 0 && kTotalChunks % kSlots == 2,
@@ -91,8 +112,8 @@ static_assert(kLdsRingOff % 16 == 0 && kSlots * kChunkB <= 65536, "ring offsets 
 constexpr int kEncWaveB = 6 * 1024;
 constexpr int kDirEncOff = 4 * 1024;
 constexpr int kLdsEncOff = kLdsRingOff + kSlots * kChunkB;
-constexpr int kLdsSegOff = kLdsEncOff + kWaves * kEncWaveB;           // fused compositing: (dist, z) per sample
-constexpr int kLdsBytes = kLdsSegOff + kWaves * kSamplesPerWave * 8;
+constexpr int kLdsSegOff = kLdsEncOff + kWaves * kCols * kEncWaveB;   // fused compositing: (dist, z) per sample
+constexpr int kLdsBytes = kLdsSegOff + kWaves * kCols * kSamplesPerWave * 8;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kFp8ScaleBytes % 16 == 0 && kLdsScaleOff % 16 == 0, "16-B aligned carve");
 
@@ -143,7 +164,14 @@ struct Ctx {
 
 // Stage this wave's pieces of the tile's chunk c (a constant after unrolling; c >= 42 is
 // the next tile's chunk c - 42, whose slot the same rotation gives).
+// NERF_FP8_ABLATE_* (timing-only lab builds, wrong results): NODMA -- the
+// stream is not restaged after the ring's first fill; NOBARRIER -- no seam barriers; NOREAD --
+// the ring's first fragments reused; NOCONV -- accumulator bits as the next layer's operands;
+// PE_ONCE -- the first tile's encodings reused.
 __device__ __forceinline__ void stage_chunk(const Ctx& cx, int c) {
+#ifdef NERF_FP8_ABLATE_NODMA
+  if (c >= kSlots) return;
+#endif
   const int slot = (c + cx.rot) & (kSlots - 1);
   const unsigned dst = cx.lds_base + unsigned(kLdsRingOff + slot * kChunkB + cx.wave_u * 1024);
   const int src = c < kTotalChunks ? c : c - kTotalChunks;
@@ -159,11 +187,13 @@ __device__ __forceinline__ void stage_chunk(const Ctx& cx, int c) {
 // c + 1 (leading half) or c + 2 (lagging half): at barrier instance k both halves stage
 // global chunk k + 1.
 __device__ __forceinline__ void seam(const Ctx& cx, int c) {
-  wait_vmcnt(0);
+  wait_vmcnt(kAhead == 2 ? kGldsPerStage : 0);
   compiler_fence();
+#ifndef NERF_FP8_ABLATE_NOBARRIER
   __builtin_amdgcn_s_barrier();
+#endif
   compiler_fence();
-  stage_chunk(cx, c + 1 + cx.lag);
+  stage_chunk(cx, c + kAhead + cx.lag);
 }
 // The seam inside the unit sequence: before unit body n when its prefetch (unit n + kPf)
 // is the first unit of a chunk.
@@ -182,7 +212,10 @@ __device__ __forceinline__ bf16x8 half8(const i32x8& v, int hi) {
 // Unit n -> ring entry n % kRing: the unit's 4 KiB as two lane-linear 32-B A operands
 // (fp8: tile o2; bf16: k-step parity s, tiles in the halves; head: k-steps 2s, 2s+1 in the
 // halves) and, for a bf16 unit on an encoding, its two bf16 B fragments.
-__device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing]) {
+__device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing][kCols]) {
+#ifdef NERF_FP8_ABLATE_NOREAD
+  if (n >= kRing) return;
+#endif
   const int s0 = (n / kChunkUnits) % kSlots;                   // the slot at rotation 0
   const unsigned addr = s0 < 2 ? cx.ring_lo : cx.ring_hi;
   const int off = s0 * kChunkB + (n % kChunkUnits) * kUnitB;
@@ -193,7 +226,10 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, i32x8 (&ra)[kRin
   const UnitInfo x = kTab.u[n];
   if (x.enc != 0) {
     const int eo = (x.enc == kPos ? 0 : kDirEncOff) + x.enc_ks * 1024;
-    rb[n % kRing] = join(ds_read_b128<i32x4>(cx.enc_addr, eo), ds_read_b128<i32x4>(cx.enc_addr, eo + 1024));
+#pragma unroll
+    for (int c = 0; c < kCols; ++c)
+      rb[n % kRing][c] = join(ds_read_b128<i32x4>(cx.enc_addr, c * kEncWaveB + eo),
+                              ds_read_b128<i32x4>(cx.enc_addr, c * kEncWaveB + eo + 1024));
   }
 }
 
@@ -209,12 +245,21 @@ __device__ __forceinline__ int cvt4(float a, float b, float c, float d) {
 __device__ __forceinline__ float relu_sat(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, kFp8Max); }
 // an accumulator tile -> half of an fp8 B operand (hid_fp8_feature order)
 __device__ __forceinline__ void convert_tile(const f32x16& t, i32x8& b, int off) {
+#ifdef NERF_FP8_ABLATE_NOCONV
+#pragma unroll
+  for (int d = 0; d < 4; ++d) b[off + d] = __builtin_bit_cast(int, t[4 * d]);
+  return;
+#endif
 #pragma unroll
   for (int d = 0; d < 4; ++d)
     b[off + d] = cvt4(relu_sat(t[4 * d]), relu_sat(t[4 * d + 1]), relu_sat(t[4 * d + 2]), relu_sat(t[4 * d + 3]));
 }
 // one quarter of that (dword d of the B operand half)
 __device__ __forceinline__ void convert_piece(const f32x16& t, i32x8& b, int off, int d) {
+#ifdef NERF_FP8_ABLATE_NOCONV
+  b[off + d] = __builtin_bit_cast(int, t[4 * d]);
+  return;
+#endif
   b[off + d] = cvt4(relu_sat(t[4 * d]), relu_sat(t[4 * d + 1]), relu_sat(t[4 * d + 2]), relu_sat(t[4 * d + 3]));
 }
 // NERF_FP8_CONV (lab knob): 1 (default) spreads each conversion over the units of its quarter
@@ -235,11 +280,16 @@ __device__ __forceinline__ unsigned cvt_relu_pair(float lo, float hi) {
 template <int N>
 __device__ __forceinline__ void bf16_dword(const f32x16 (&acc)[8], int t, int m, u32x4 (&f)[N]) {
   const int tile = t + (m >> 3), pr = m & 7;
+#ifdef NERF_FP8_ABLATE_NOCONV
+  f[2 * tile + (pr >> 2)][pr & 3] = __builtin_bit_cast(unsigned, acc[tile][2 * pr]);
+  return;
+#endif
   f[2 * tile + (pr >> 2)][pr & 3] = cvt_relu_pair(acc[tile][2 * pr], acc[tile][2 * pr + 1]);
 }
 
 // NERF_FP8_SCHED (lab knob): an explicit issue pattern for a unit body's scheduling region
-// (sched_group_barrier), per MFMA: 1: 1 MFMA, 2 VALU, 1 DS read; 2: 1 MFMA, 1 DS read, 3 VALU.
+// (sched_group_barrier), per MFMA: 1: 1 MFMA, 2 VALU, 1 DS read; 2: 1 MFMA, 1 DS read, 3 VALU;
+// 3: 1 MFMA, 1 DS read, 6 VALU; 4: 1 MFMA, 3 VALU, 1 DS read, 3 VALU.
 #ifndef NERF_FP8_SCHED
 #define NERF_FP8_SCHED 0
 #endif
@@ -254,6 +304,15 @@ __device__ __forceinline__ void sched_unit_pattern(int n_mfma) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+    } else if (NERF_FP8_SCHED == 3) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+    } else if (NERF_FP8_SCHED == 4) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
     }
   }
 }
@@ -265,8 +324,9 @@ NL_HD bool in_b16(int l) { return l == L1 || l == C0; }     // hidden input from
 NL_HD bool in_f8(int l) { return !mix_bf16_layer(l); }      // hidden input from an fp8 set
 
 template <int L>
-__device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i32x8 (&b8out)[4], u32x4 (&b16)[16],
-                                          u32x4 (&hb)[8], i32x8 (&ra)[kRing][2], i32x8 (&rb)[kRing], const Ctx& cx) {
+__device__ __forceinline__ void layer_mix(f32x16 (&acc)[kCols][8], i32x8 (&b8in)[kCols][4], i32x8 (&b8out)[kCols][4],
+                                          u32x4 (&b16)[kCols][16], u32x4 (&hb)[kCols][8], i32x8 (&ra)[kRing][2],
+                                          i32x8 (&rb)[kRing][kCols], const Ctx& cx) {
   constexpr int UPQ = mix_units_per_quarter(L);
   constexpr int NF = mix_f8_units(L);
   constexpr int NQ = out_tiles(L) / 2;
@@ -287,8 +347,10 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
           const int off = 4 * (kBiasOff + 256 * L + (2 * q + o2) * 32);
           const f32x4 b0 = ds_read_b128<f32x4>(cx.bias_addr, off), b1 = ds_read_b128<f32x4>(cx.bias_addr, off + 16);
           const f32x4 b2 = ds_read_b128<f32x4>(cx.bias_addr, off + 32), b3 = ds_read_b128<f32x4>(cx.bias_addr, off + 48);
-          acc[2 * q + o2] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                                   b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+          const f32x16 bias = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                     b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) acc[c][2 * q + o2] = bias;
         }
         if (NF > 0) {
           const u32x2 sc = ds_read_b64(cx.scale_addr, (L * 4 + q) * 512);
@@ -299,21 +361,28 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
       wait_lgkm(0);
       if (u < NF) {                                   // fp8 k-step u over the fp8 set
-        acc[2 * q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][0], b8in[u < NF ? u : 0], acc[2 * q],
-                                                                    0, 0, 0, sa0, 0, 127);
-        acc[2 * q + 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][1], b8in[u < NF ? u : 0],
-                                                                        acc[2 * q + 1], 0, 0, 0, sa1, 0, 127);
+#pragma unroll
+        for (int c = 0; c < kCols; ++c)
+          acc[c][2 * q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][0], b8in[c][u < NF ? u : 0],
+                                                                       acc[c][2 * q], 0, 0, 0, sa0, 0, 127);
+#pragma unroll
+        for (int c = 0; c < kCols; ++c)
+          acc[c][2 * q + 1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ra[n % kRing][1], b8in[c][u < NF ? u : 0],
+                                                                           acc[c][2 * q + 1], 0, 0, 0, sa1, 0, 127);
       } else {                                        // two bf16 k-steps
         const int b = u - NF;
         const bool enc = kTab.u[n].enc != 0;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int ks = 2 * b + s;                   // hidden k-step (bf16 layers' hidden units)
-          const bf16x8 bf = enc ? half8(rb[n % kRing], s) : __builtin_bit_cast(bf16x8, b16[ks < 16 ? ks : 0]);
 #pragma unroll
           for (int o2 = 0; o2 < 2; ++o2)
-            acc[2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(half8(ra[n % kRing][s], o2), bf, acc[2 * q + o2],
-                                                                     0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < kCols; ++c) {
+              const bf16x8 bf = enc ? half8(rb[n % kRing][c], s) : __builtin_bit_cast(bf16x8, b16[c][ks < 16 ? ks : 0]);
+              acc[c][2 * q + o2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(half8(ra[n % kRing][s], o2), bf,
+                                                                          acc[c][2 * q + o2], 0, 0, 0);
+            }
         }
       }
       // the previous layer's tiles 6, 7 -> this layer's input, before its unit reads them
@@ -321,16 +390,23 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
         if (NERF_FP8_CONV) {   // 8 pieces over units 1, 2 (unit 3 reads them)
 #pragma unroll
           for (int pc = 0; pc < 8; ++pc)
-            if (1 + pc / 4 == u) convert_piece(acc[6 + (pc >> 2)], b8in[3], 4 * (pc >> 2), pc & 3);
+            if (1 + pc / 4 == u)
+#pragma unroll
+              for (int c = 0; c < kCols; ++c) convert_piece(acc[c][6 + (pc >> 2)], b8in[c][3], 4 * (pc >> 2), pc & 3);
         } else {
-          if (u == 1) convert_tile(acc[6], b8in[3], 0);
-          if (u == 2) convert_tile(acc[7], b8in[3], 4);
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) {
+            if (u == 1) convert_tile(acc[c][6], b8in[c][3], 0);
+            if (u == 2) convert_tile(acc[c][7], b8in[c][3], 4);
+          }
         }
       }
       if (q == 0 && in_b16(L)) {
 #pragma unroll
         for (int m = 0; m < 16; ++m)   // k-steps 12..15 are read by unit 6
-          if ((NERF_FP8_CONV ? 1 + (m * 5) / 16 : (m * 6) / 16) == u) bf16_dword(acc, 6, m, b16);
+          if ((NERF_FP8_CONV ? 1 + (m * 5) / 16 : (m * 6) / 16) == u)
+#pragma unroll
+            for (int c = 0; c < kCols; ++c) bf16_dword(acc[c], 6, m, b16[c]);
       }
       // this layer's final tiles 2q-2, 2q-1 -> the next layer's operand type
       if (q >= 1) {
@@ -339,23 +415,31 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
 #pragma unroll
             for (int pc = 0; pc < 8; ++pc)
               if (1 + (pc * (UPQ - 1)) / 8 == u)
-                convert_piece(acc[2 * q - 2 + (pc >> 2)], b8out[q >= 1 ? q - 1 : 0], 4 * (pc >> 2), pc & 3);
+#pragma unroll
+                for (int c = 0; c < kCols; ++c)
+                  convert_piece(acc[c][2 * q - 2 + (pc >> 2)], b8out[c][q >= 1 ? q - 1 : 0], 4 * (pc >> 2), pc & 3);
           } else {
-            if (u == 1) convert_tile(acc[2 * q - 2], b8out[q >= 1 ? q - 1 : 0], 0);
-            if (u == 2) convert_tile(acc[2 * q - 1], b8out[q >= 1 ? q - 1 : 0], 4);
+#pragma unroll
+            for (int c = 0; c < kCols; ++c) {
+              if (u == 1) convert_tile(acc[c][2 * q - 2], b8out[c][q >= 1 ? q - 1 : 0], 0);
+              if (u == 2) convert_tile(acc[c][2 * q - 1], b8out[c][q >= 1 ? q - 1 : 0], 4);
+            }
           }
         } else if (OUT == kOutB16) {
 #pragma unroll
           for (int m = 0; m < 16; ++m)
             if ((NERF_FP8_CONV ? (UPQ - 1) - ((15 - m) * (UPQ - 1)) / 16 : (m * UPQ) / 16) == u)
-              bf16_dword(acc, 2 * q - 2, m, b16);
+#pragma unroll
+              for (int c = 0; c < kCols; ++c) bf16_dword(acc[c], 2 * q - 2, m, b16[c]);
         } else {   // C0's tiles 0, 1 -> colour k-steps 16..19 (its tiles 2, 3 in the head units)
 #pragma unroll
           for (int m = 0; m < 16; ++m)
-            if ((NERF_FP8_CONV ? 1 + (m * (UPQ - 1)) / 16 : (m * UPQ) / 16) == u) bf16_dword(acc, 0, m, hb);
+            if ((NERF_FP8_CONV ? 1 + (m * (UPQ - 1)) / 16 : (m * UPQ) / 16) == u)
+#pragma unroll
+              for (int c = 0; c < kCols; ++c) bf16_dword(acc[c], 0, m, hb[c]);
         }
       }
-      if (NERF_FP8_SCHED) sched_unit_pattern(u < NF ? 2 : 4);
+      if (NERF_FP8_SCHED) sched_unit_pattern(kCols * (u < NF ? 2 : 4));
     }
   }
 }
@@ -363,14 +447,16 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[8], i32x8 (&b8in)[4], i3
 // This tile's sample inputs -> its encodings in the wave's own LDS slots (bf16), and for
 // fused compositing the integral's network-independent inputs.
 template <bool kExplicit>
-__device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src, long p, long n_points, bool fused) {
+__device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src, long p, long n_points, bool fused,
+                                            int col) {
   float x[3], d[3], pef[32], def[16];
   float dist = 0.0f, zz = 0.0f;
   if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
   else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, fused, x, d, dist, zz);
   pos_encode<true>(x[0], x[1], x[2], cx.h, pef);
   dir_encode<true>(d[0], d[1], d[2], cx.h, def);
-  char* dst = cx.lds + kLdsEncOff + cx.wave_u * kEncWaveB + cx.lane * 16;
+  const int slot = cx.wave_u * kCols + col;                 // the column's encoding and segment slots
+  char* dst = cx.lds + kLdsEncOff + slot * kEncWaveB + cx.lane * 16;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     bf16x8 v;
@@ -386,7 +472,7 @@ __device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src,
     *(bf16x8*)(dst + kDirEncOff + u * 1024) = v;
   }
   if (!kExplicit && fused && cx.h == 0)
-    *(f32x2_t*)(cx.lds + kLdsSegOff + (cx.wave_u * kSamplesPerWave + (cx.lane & 31)) * 8) = f32x2_t{dist, zz};
+    *(f32x2_t*)(cx.lds + kLdsSegOff + (slot * kSamplesPerWave + (cx.lane & 31)) * 8) = f32x2_t{dist, zz};
 }
 
 // A tile's outputs, stored after the next tile's first seam: vmcnt counts stores together
@@ -418,10 +504,10 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   f32x4* const dst = fused ? seg : out;
   Ctx cx0{blob, lds, base, wave_u, lane, h,
           base + kLdsRingOff + lane * 16, base + kLdsRingOff + lane * 16,
-          base + kLdsEncOff + wave_u * kEncWaveB + lane * 16,
+          base + kLdsEncOff + wave_u * kCols * kEncWaveB + lane * 16,
           base + kLdsParamOff + h * 64,
           base + kLdsScaleOff + lane * 8,
-          0, wave_u >= kWaves / 2 ? 1 : 0};
+          0, kLag && wave_u >= kWaves / 2 ? 1 : 0};
 
   // The stream's first two chunks, and the parameters and row scales, once per workgroup.
   stage_chunk(cx0, 0);
@@ -431,7 +517,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
   for (int i = threadIdx.x; i < kFp8ScaleBytes / 16; i += kThreads)
     ((f32x4*)(lds + kLdsScaleOff))[i] = ((const f32x4*)(blob + kFp8ScaleOff))[i];
   const float* prm = (const float*)(lds + kLdsParamOff);
-  Pending pd;
+  Pending pd[kCols];
 
 #pragma unroll 1
   for (long tile = blockIdx.x, it = 0; tile < n_tiles; tile += gridDim.x, ++it) {
@@ -442,27 +528,33 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     cx.rot = int(it & 1) * 2;
     cx.ring_lo = cx0.ring_lo + unsigned(cx.rot * kChunkB);
     cx.ring_hi = cx0.ring_hi - unsigned(cx.rot * kChunkB);
-    const long p = (tile * kWaves + wave_u) * kSamplesPerWave + (lane & 31);
+    const long p = (tile * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
     // this tile's encodings into the wave's own slots (its reads of the previous tile's
     // were consumed by that tile's MFMAs)
-    encode_tile<kExplicit>(cx, src, p, n_points, fused);
+#ifdef NERF_FP8_ABLATE_PE_ONCE
+    if (it == 0)
+#endif
+#pragma unroll 1
+    for (int c = 0; c < kCols; ++c) encode_tile<kExplicit>(cx, src, p + c * kSamplesPerWave, n_points, fused, c);
     if (it == 0) {
       // barrier instance 0 publishes chunk 0 (and the parameters); the lagging half then
       // takes its seam for chunk 0 (instance 1, staging chunk 2)
       wait_vmcnt(kGldsPerStage);                     // own pieces of chunk 0 (chunk 1 may be in flight)
       __syncthreads();
       if (cx.lag) seam(cx, 0);
+      if (kAhead == 2) stage_chunk(cx, 2);           // what the tile-top seam stages on later tiles
     } else {
       seam(cx, 0);
-      store_pending(pd, dst, wloc);                  // the previous tile's outputs
+#pragma unroll
+      for (int c = 0; c < kCols; ++c) store_pending(pd[c], dst, wloc);   // the previous tile's outputs
     }
-    i32x8 ra[kRing][2], rb[kRing];
+    i32x8 ra[kRing][2], rb[kRing][kCols];
 #pragma unroll
     for (int n = 0; n < kPf; ++n) read_unit(cx, n, ra, rb);
 
-    f32x16 acc[8];
-    u32x4 b16[16], hb[8];
-    i32x8 bA[4], bB[4];                              // the fp8 sets: a layer reads one, fills the other
+    f32x16 acc[kCols][8];
+    u32x4 b16[kCols][16], hb[kCols][8];
+    i32x8 bA[kCols][4], bB[kCols][4];                // the fp8 sets: a layer reads one, fills the other
     layer_mix<L0>(acc, bA, bB, b16, hb, ra, rb, cx);   // bf16: PE -> b16
     layer_mix<L1>(acc, bB, bA, b16, hb, ra, rb, cx);   // bf16: b16 -> fp8 bA
     layer_mix<L2>(acc, bA, bB, b16, hb, ra, rb, cx);
@@ -476,12 +568,16 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     // Heads (nerf.py:114, 123-129) as one bf16 MFMA tile: row 3 density over L7's output
     // (b16, k-steps 0..15), rows 0-2 colour over C0's output (hb, k-steps 16..23; C0's
     // tiles 2, 3 converted during the density units).
-    f32x16 hacc = f32x16{};
-    if (h == 0) {
-      hacc[0] = prm[kC1B];
-      hacc[1] = prm[kC1B + 1];
-      hacc[2] = prm[kC1B + 2];
-      hacc[3] = prm[kSigB];
+    f32x16 hacc[kCols];
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      hacc[c] = f32x16{};
+      if (h == 0) {
+        hacc[c][0] = prm[kC1B];
+        hacc[c][1] = prm[kC1B + 1];
+        hacc[c][2] = prm[kC1B + 2];
+        hacc[c][3] = prm[kSigB];
+      }
     }
 #pragma unroll
     for (int i = 0; i < kMixHeadUnits; ++i) {
@@ -492,42 +588,53 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ks = 4 * i + k;
-        const bf16x8 bf = __builtin_bit_cast(bf16x8, ks < 16 ? b16[ks < 16 ? ks : 0] : hb[ks >= 16 ? ks - 16 : 0]);
-        hacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(half8(ra[n % kRing][k >> 1], k & 1), bf, hacc, 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) {
+          const bf16x8 bf = __builtin_bit_cast(bf16x8, ks < 16 ? b16[c][ks < 16 ? ks : 0] : hb[c][ks >= 16 ? ks - 16 : 0]);
+          hacc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(half8(ra[n % kRing][k >> 1], k & 1), bf, hacc[c], 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int m = 0; m < 16; ++m)
-        if (i < 4 && m / 4 == i) bf16_dword(acc, 2, m, hb);   // C0's tiles 2, 3 -> k-steps 20..23
+        if (i < 4 && m / 4 == i)
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) bf16_dword(acc[c], 2, m, hb[c]);   // C0's tiles 2, 3 -> k-steps 20..23
+      if (NERF_FP8_SCHED) sched_unit_pattern(4 * kCols);
     }
     // the sample index again, from the lane id recounted by v_mbcnt: keeping the 64-bit p
     // (or the lane id) live through the layers costs a spill, and its reload a vmcnt(0)
     // drain of the weight stream
     const int lane_o = int(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
-    const long p_o = (tile * kWaves + wave_u) * kSamplesPerWave + (lane_o & 31);
-    const f32x4 res{relu(hacc[3]), sigmoid_ref(hacc[0]), sigmoid_ref(hacc[1]), sigmoid_ref(hacc[2])};
-    pd = Pending{};
-    if (fused) {                                       // fused compositing: one record per segment
-      const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + (wave_u * kSamplesPerWave + (lane_o & 31)) * 8);
-      float wl;
-      pd.v = seg_composite(res, in[0], in[1], lane_o, wl);
-      const long first = p_o - (lane_o & 31);
-      if (first < n_points && lane_o < 2) pd.idx = (first / kSamplesPerWave) * 2 + lane_o;
-      if (wloc != nullptr && p_o < n_points && h == 0) {
-        pd.wl = wl;
-        pd.widx = p_o;
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      const long p_o = (tile * kWaves + wave_u) * (kCols * kSamplesPerWave) + c * kSamplesPerWave + (lane_o & 31);
+      const f32x4 res{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
+      pd[c] = Pending{};
+      if (fused) {                                       // fused compositing: one record per segment
+        const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff +
+                                             ((wave_u * kCols + c) * kSamplesPerWave + (lane_o & 31)) * 8);
+        float wl;
+        pd[c].v = seg_composite(res, in[0], in[1], lane_o, wl);
+        const long first = p_o - (lane_o & 31);
+        if (first < n_points && lane_o < 2) pd[c].idx = (first / kSamplesPerWave) * 2 + lane_o;
+        if (wloc != nullptr && p_o < n_points && h == 0) {
+          pd[c].wl = wl;
+          pd[c].widx = p_o;
+        }
+      } else if (p_o < n_points && h == 0) {
+        pd[c].v = res;
+        pd[c].idx = p_o;
       }
-    } else if (p_o < n_points && h == 0) {
-      pd.v = res;
-      pd.idx = p_o;
     }
   }
   // the leading half's matching barrier for the lagging half's last seam
-  if (!cx0.lag) {
+  if (kLag && !cx0.lag) {
     compiler_fence();
     __builtin_amdgcn_s_barrier();
     compiler_fence();
   }
-  store_pending(pd, dst, wloc);
+#pragma unroll
+  for (int c = 0; c < kCols; ++c) store_pending(pd[c], dst, wloc);
   // the stream ran two chunks into a tile that does not exist: let them land before the
   // workgroup's LDS is released
   wait_vmcnt(0);

@@ -249,6 +249,16 @@ __device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
   }
 }
 
+// NERF_X3_ABLATE_NODIR (timing-only lab build, wrong results): C0's direction k-steps, their
+// B-fragment reads and the per-sample direction encoding dropped -- the upper bound of
+// computing Wc0[:, 256:283] . PE4(d) once per ray instead of per sample (VERDICT r5 next 5a:
+// nerf.py:117-129 feeds one PE4(d) to all samples of a ray).
+#ifdef NERF_X3_ABLATE_NODIR
+constexpr bool kNoDir = true;
+#else
+constexpr bool kNoDir = false;
+#endif
+
 // Reads of unit n into ring entry n % kRing: A_hi and A_lo of the unit's two
 // output tiles and, for encoding inputs, the B fragment's hi and lo.
 template <class Op, class F = typename Op::frag>
@@ -262,7 +272,7 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, F (&ra)[kRing][4
 #pragma unroll
   for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<F>(base, off + f * 1024);
   const int ex = kTab.u[n].extra;
-  if (ex != 0) {
+  if (ex != 0 && !(kNoDir && ex == kDir)) {
     const int u = kTab.u[n].kstep - layer_shape(kTab.u[n].layer).hidden / 16;
     if (ex == kPos) {
       rb[n % kRing][0] = ds_read_b128<F>(cx.pe_addr, u * 1024);
@@ -542,9 +552,10 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
       const bool hid = u < KH;
       const F bhi = hid ? __builtin_bit_cast(F, ih[hid ? u : 0]) : rb[n % kRing][0];
       const F blo = hid ? __builtin_bit_cast(F, il[hid ? u : 0]) : rb[n % kRing][1];
+      if (!(kNoDir && L == C0 && !hid))
 #pragma unroll
-      for (int o2 = 0; o2 < 2; ++o2)
-        acc[2 * q + o2] = mfma3<Op>(ra[n % kRing][o2], ra[n % kRing][2 + o2], bhi, blo, acc[2 * q + o2]);
+        for (int o2 = 0; o2 < 2; ++o2)
+          acc[2 * q + o2] = mfma3<Op>(ra[n % kRing][o2], ra[n % kRing][2 + o2], bhi, blo, acc[2 * q + o2]);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int t = m >> 3, pr = m & 7;
@@ -635,7 +646,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
         fetch_sample<kExplicit>(src, pc, x, d);
       }
       pos_encode<false, kTrain>(x[0], x[1], x[2], h, pef);    // accurate sin/cos, as the fp32 path
-      dir_encode<false, kTrain>(d[0], d[1], d[2], h, def);
+      if (!kNoDir) dir_encode<false, kTrain>(d[0], d[1], d[2], h, def);
       char* pe_dst = lds + kLdsPeOff + wave_u * kPeWaveB + lane * 16;
       char* de_dst = lds + kLdsDeOff + wave_u * kDeWaveB + lane * 16;
 #pragma unroll
@@ -646,7 +657,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
         *(u32x4*)(pe_dst + 4096 + u * 1024) = lo;
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < (kNoDir ? 0 : 2); ++u) {
         u32x4 hi, lo;
         split8<Op>(def + 8 * u, hi, lo);
         *(u32x4*)(de_dst + u * 1024) = hi;

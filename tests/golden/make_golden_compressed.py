@@ -4,6 +4,7 @@ Run in the development container only (the reference is not on the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_compressed.py [/root/reference]
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_compressed.py --lego [/root/reference]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_compressed.py --lego-full [/root/reference]
 
 Imports src/benchmark/compressed_renderer.py (default config: 10 % magnitude
 pruning and int8 asymmetric per-tensor quantisation of every weight and bias,
@@ -14,6 +15,12 @@ the same deterministic synthetic checkpoint as make_golden.py, and records:
   compressed_lego.npz (--lego)  render_image on the distilled Lego checkpoint at
                   200x150, 32 samples, suite view 0 and the off-axis pose of make_golden.py:
                   config 5's error baseline on the content BASELINE names.
+  compressed_lego_800x600_s128.npz (--lego-full)  the same renderer on whole 800x600x128
+                  frames (config 5's own size), suite view 0 and the off-axis pose, through its
+                  own generate_rays / sample_points_on_rays / query_nerf_networks /
+                  execute_volume_rendering in 4096-ray chunks (render_image in one piece would
+                  hold 61 M samples' activations); the chunking is first checked to reproduce
+                  render_image bit for bit at 200x150x32.
 These pin the oracle's restatement (oracle/nerf_oracle.py, compressed_*), which
 is the error baseline the fp8 path is reported against; the reference's
 compressed renderer is not a parity target.
@@ -69,6 +76,62 @@ def main_lego(ref_root: str = "/root/reference") -> None:
     print("compressed_lego.npz:", out["rgb_0"].shape)
 
 
+def _render_chunked(r, pose, width, height, spp, chunk=4096):
+    """CompressedNeRFRenderer.render_image (compressed_renderer.py:311-358) over ray chunks:
+    its own pieces, in its order, on `chunk` rays at a time."""
+    import torch
+
+    rays_o, rays_d = r.generate_rays(pose, width, height)
+    ro, rd = rays_o.reshape(-1, 3), rays_d.reshape(-1, 3)
+    rgbs, depths = [], []
+    with torch.no_grad():
+        for c in range(0, ro.shape[0], chunk):
+            o, d = ro[c:c + chunk], rd[c:c + chunk]
+            pts, z = r.sample_points_on_rays(o, d, spp)
+            dirs = d.unsqueeze(1).expand(-1, spp, -1).reshape(-1, 3)
+            sig, col = r.query_nerf_networks(pts.reshape(-1, 3), dirs)
+            rgb, depth = r.execute_volume_rendering(sig.reshape(o.shape[0], spp, -1), col.reshape(o.shape[0], spp, 3),
+                                                    z, d)
+            rgbs.append(rgb.float())
+            depths.append(depth.float())
+    return torch.cat(rgbs).reshape(height, width, 3), torch.cat(depths).reshape(height, width)
+
+
+def main_lego_full(ref_root: str = "/root/reference") -> None:
+    """Config 5's error baseline at config 5's size: whole 800x600x128
+    frames of the reference's int8 renderer on the Lego checkpoint."""
+    import time
+
+    import torch
+
+    sys.path.insert(0, HERE)
+    from make_golden import off_axis_pose, suite_poses
+
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    CompressedNeRFRenderer = _import(ref_root)
+    ckpt = W.write_lego_checkpoint(os.path.join(tempfile.mkdtemp(), "lego.pth"))
+    r = CompressedNeRFRenderer()
+    r.setup(ckpt)
+    poses = [suite_poses(2)[0], off_axis_pose()]
+    # the chunked form against render_image itself, bit for bit, at 200x150x32 (both poses)
+    g = np.load(os.path.join(HERE, "compressed_lego.npz"))
+    for k, p in enumerate(poses):
+        with torch.no_grad():
+            img, depth = r.render_image(p, (200, 150), 32)
+        ci, cd = _render_chunked(r, p, 200, 150, 32, chunk=4096)
+        assert torch.equal(img.float(), ci) and torch.equal(depth.float(), cd), "chunking changes the render"
+        assert np.array_equal(g[f"rgb_{k}"], ci.numpy()) and np.array_equal(g[f"depth_{k}"], cd.numpy())
+    print("chunked render == render_image at 200x150x32 on both poses", flush=True)
+    out = {"poses": np.stack([p.numpy() for p in poses]), "pose_ids": np.array([0, 2], dtype=np.int32),
+           "W": np.int32(800), "H": np.int32(600), "S": np.int32(128), "chunk_rays": np.int32(4096)}
+    for k, p in enumerate(poses):
+        t0 = time.time()
+        rgb, depth = _render_chunked(r, p, 800, 600, 128)
+        out[f"rgb_{k}"], out[f"depth_{k}"] = rgb.numpy(), depth.numpy()
+        print(f"view {k}: {time.time() - t0:.0f} s", flush=True)
+    np.savez_compressed(os.path.join(HERE, "compressed_lego_800x600_s128.npz"), **out)
+
+
 def main(ref_root: str = "/root/reference") -> None:
     import torch
 
@@ -98,4 +161,7 @@ def main(ref_root: str = "/root/reference") -> None:
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    (main_lego if "--lego" in sys.argv else main)(args[0] if args else "/root/reference")
+    if "--lego-full" in sys.argv:
+        main_lego_full(args[0] if args else "/root/reference")
+    else:
+        (main_lego if "--lego" in sys.argv else main)(args[0] if args else "/root/reference")
