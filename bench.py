@@ -426,6 +426,27 @@ def errors_vs_reference(r, which="headline"):
     return out
 
 
+def int8_renderer_error():
+    """The reference's int8 CompressedNeRFRenderer (compressed_renderer.py:161-358) on whole
+    800x600x128 Lego frames against the reference's fp32 render, from the two fixtures
+    (make_golden_compressed.py --lego-full, make_golden.py --lego-full): config 5's error bar,
+    beside the fp8 line's own error on the same views."""
+    import numpy as np
+
+    pc, pf = os.path.join(GOLDEN, "compressed_lego_800x600_s128.npz"), os.path.join(GOLDEN, FIXTURES["headline"])
+    if not (os.path.exists(pc) and os.path.exists(pf)):
+        return {"error": "fixture missing"}
+    gc, g = np.load(pc), np.load(pf)
+    views = []
+    for kc, pid in enumerate(gc["pose_ids"]):
+        kg = int(np.flatnonzero(g["pose_ids"] == pid)[0])
+        e = np.abs(gc[f"rgb_{kc}"] - g[f"rgb_{kg}"])
+        d = np.abs(gc[f"depth_{kc}"] - g[f"depth_{kg}"])
+        views.append({"pose_id": int(pid), "rgb_max_abs": float(e.max()), "rgb_mean_abs": float(e.mean()),
+                      "depth_pixels_gt_1e-2": int((d > 1e-2).sum())})
+    return {"reference": os.path.relpath(pc, REPO), "views": views}
+
+
 def other_configs(ckpt, poses, local, ref32):
     """The BASELINE configs besides the headline, 1 GPU each, each on the
     suite's two views (rays/s = W*H / mean view time): C2 400x300x64 fp32 (the parity
@@ -522,6 +543,23 @@ def other_configs(ckpt, poses, local, ref32):
         "pixels_over_1e-4": errh3.get("pixels_over_1e-4"), "vs_fp64": errh3.get("vs_fp64"),
         "depth_pixels_gt_1e-2": errh3.get("depth_pixels_gt_1e-2"), "error_vs_reference": errh3}
     del h3
+    # the same with the coarse pass on the fp32 path (NERF_OPT_COARSE_PRECISION): the sampler then
+    # sees the fp32 path's coarse weights, and the render is as close to the float64 chain as the
+    # fp32 path's (tests/test_gpu_lego_c3.py (iv))
+    h3c = MI355XRenderer("f16x3", n_importance=128, device_index=local, coarse_precision="fp32")
+    h3c.setup(ckpt)
+    h3c.hip.set_profiling(True)
+    step, _ = frame_step(h3c, poses, 800, 600, 64, 0, 1)
+    dt = time_steps(step, 1, 1, 1) / nv
+    st = h3c.hip.stage_ms()
+    h3c.check_range()
+    errh3c = errors_vs_reference(h3c, "c3")
+    out["c3_hierarchical_f16x3_fp32coarse_800x600_64+128"] = {
+        "rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "stage_ms_last_view": st,
+        "rgb_max_abs_vs_reference": errh3c.get("rgb_max_abs_vs_reference"),
+        "pixels_over_1e-4": errh3c.get("pixels_over_1e-4"), "vs_fp64": errh3c.get("vs_fp64"),
+        "depth_pixels_gt_1e-2": errh3c.get("depth_pixels_gt_1e-2"), "error_vs_reference": errh3c}
+    del h3c
 
     f8 = MI355XRenderer("fp8", device_index=local)
     f8.setup(ckpt)
@@ -540,7 +578,8 @@ def other_configs(ckpt, poses, local, ref32):
                         f"ceiling {FP8_MIX_CEILING:.0f} TFLOP/s for this mix",
         "rgb_max_abs_vs_reference": err8.get("rgb_max_abs_vs_reference"),
         "rgb_mean_abs_vs_reference": err8.get("rgb_mean_abs_vs_reference"),
-        "depth_pixels_gt_1e-2": err8.get("depth_pixels_gt_1e-2"), "error_vs_reference": err8}
+        "depth_pixels_gt_1e-2": err8.get("depth_pixels_gt_1e-2"), "error_vs_reference": err8,
+        "int8_compressed_renderer_vs_reference": int8_renderer_error()}
     return out, f8
 
 

@@ -243,6 +243,13 @@ int nerf_ctx_stage_ms_history(nerf_ctx* ctx, int n, float* ms_out /* [n][NERF_N_
  *   hierarchical coarse pass, whose weights then come from the MLP epilogue. 0 writes
  *   (sigma, rgb) per sample and runs the sequential composite kernel for both. */
 #define NERF_OPT_FUSED_COMPOSITE 1
+/*   NERF_OPT_COARSE_PRECISION (default -1: the render's own precision): the precision of the
+ *   hierarchical coarse pass (rendering.py:54-100's first network evaluation) when it should
+ *   differ from the fine pass's, e.g. NERF_FP32 under an NERF_F16X3 render.  The importance
+ *   sampler turns last-bit differences of the coarse weights into moved fine samples at a few
+ *   hundred rays per 800x600 frame, so the coarse pass's accumulation sets how close a
+ *   hierarchical render is to the float64 result of the same chain. */
+#define NERF_OPT_COARSE_PRECISION 2
 int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value);
 
 /* ---------------------------------------------------------------------------------------

@@ -82,6 +82,7 @@ struct nerf_ctx {
   int last_zfine_per_ray = 0;
   bool profiling = false;
   int fused_composite = 3;     // NERF_OPT_FUSED_COMPOSITE bits: 1 render passes, 2 hierarchical coarse pass
+  int coarse_precision = -1;   // NERF_OPT_COARSE_PRECISION: -1 = the render's precision
   // stage events of the last kEvFrames renders (a ring, so that per-frame stage
   // times can be read after a run of back-to-back renders without a host sync each)
   struct Frame {
@@ -341,6 +342,13 @@ int nerf_ctx_set_option(nerf_ctx* ctx, int option, int value) {
     ctx->fused_composite = value;
     return NERF_OK;
   }
+  if (option == NERF_OPT_COARSE_PRECISION) {
+    if (value != -1 && value != NERF_FP32 && value != NERF_BF16 && value != NERF_FP8 && value != NERF_BF16X3 &&
+        value != NERF_F16X3)
+      return set_error(NERF_E_INVALID, "NERF_OPT_COARSE_PRECISION takes -1 or a precision, got %d", value);
+    ctx->coarse_precision = value;
+    return NERF_OK;
+  }
   return set_error(NERF_E_INVALID, "unknown option %d", option);
 }
 
@@ -389,9 +397,10 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
                 const float* t_rand, const float* u_rays, int precision, float* rgb_out, float* depth_out,
                 OutStrides os, void* stream) {
   const int net_main = NERF_NET_FINE;
+  const int coarse_prec = ctx->coarse_precision >= 0 ? ctx->coarse_precision : precision;
   int rc = check_net(ctx, net_main, precision);
   if (rc != NERF_OK) return rc;
-  if (n_importance > 0 && (rc = check_net(ctx, NERF_NET_COARSE, precision)) != NERF_OK) return rc;
+  if (n_importance > 0 && (rc = check_net(ctx, NERF_NET_COARSE, coarse_prec)) != NERF_OK) return rc;
   if (!c2w || !t_vals) return set_error(NERF_E_INVALID, "nerf_render: null argument");
   if (width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 > row1)
     return set_error(NERF_E_INVALID, "nerf_render: bad image/rows %dx%d [%d,%d)", width, height, row0, row1);
@@ -489,11 +498,11 @@ int render_impl(nerf_ctx* ctx, const float* c2w, int width, int height, int row0
     // sampler scales them by the earlier segments' transmittance; otherwise the
     // (sigma, rgb) buffer and the sequential composite kernel (the coarse image
     // itself is not an output of render_image)
-    const bool fuse_coarse = (ctx->fused_composite & 2) && (precision == NERF_BF16 || precision == NERF_FP8) &&
+    const bool fuse_coarse = (ctx->fused_composite & 2) && (coarse_prec == NERF_BF16 || coarse_prec == NERF_FP8) &&
                              n_samples % 32 == 0 &&
                              n_importance <= 1024;
     SampleSrc src{rays_o, rays_d, z_first, z_first_stride, n_samples, nullptr, nullptr};
-    HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, precision, src, n_rays * n_samples, ctx->mlp_out, false, s,
+    HIP_TRY(run_mlp(ctx, NERF_NET_COARSE, coarse_prec, src, n_rays * n_samples, ctx->mlp_out, false, s,
                     fuse_coarse ? ctx->mlp_out : nullptr, fuse_coarse ? d_w : nullptr));
     fr.ran[1] = true;
     if ((rc = mark(2)) != NERF_OK) return rc;

@@ -53,14 +53,17 @@ class MI355XRenderer(BaseUnifiedRenderer):
     fp32 accumulate; the throughput path).  n_importance > 0 turns on the
     build-defined hierarchical mode: ``samples_per_ray`` coarse samples on the
     coarse net, ``n_importance`` inverse-CDF samples, fine net on the sorted
-    union.
+    union.  ``coarse_precision`` runs that coarse pass at another precision
+    than the fine pass (e.g. "fp32" under "f16x3": the sampler amplifies the coarse weights'
+    rounding, so the coarse pass's accumulation sets how close the render is to the float64
+    result of the same chain; include/nerf_mi355x.h NERF_OPT_COARSE_PRECISION).
     """
 
     def __init__(self, precision: str = "bf16", n_importance: int = 0, device_index: Optional[int] = None,
-                 name: Optional[str] = None):
+                 name: Optional[str] = None, coarse_precision: Optional[str] = None):
         import torch
 
-        if precision not in rt.PRECISIONS:
+        if precision not in rt.PRECISIONS or (coarse_precision is not None and coarse_precision not in rt.PRECISIONS):
             raise ValueError(f"precision must be one of {sorted(rt.PRECISIONS)}")
         if not torch.cuda.is_available():
             raise RuntimeError("no ROCm/HIP device available")
@@ -69,9 +72,14 @@ class MI355XRenderer(BaseUnifiedRenderer):
         self.device_index = idx
         self.precision = precision
         self.n_importance = int(n_importance)
+        self.coarse_precision = coarse_precision
+        if coarse_precision is not None:
+            self.hip.set_coarse_precision(rt.PRECISIONS[coarse_precision])
         self.focal = FOCAL
         if name is None:
             name = f"MI355X HIP {precision}" + (f" hier+{self.n_importance}" if self.n_importance else "")
+            if coarse_precision is not None and self.n_importance:
+                name += f" ({coarse_precision} coarse)"
         super().__init__(name, "cuda")
         self._u_cache = {}
 

@@ -29,6 +29,7 @@ NERF_NET_COARSE, NERF_NET_FINE = 0, 1
 NERF_N_PARAMS = 22
 NERF_N_STAGES = 5
 NERF_OPT_FUSED_COMPOSITE = 1
+NERF_OPT_COARSE_PRECISION = 2
 STAGES = ("rays", "coarse_mlp", "importance", "fine_mlp", "composite")
 
 PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16, "fp8": NERF_FP8, "bf16x3": NERF_BF16X3, "f16x3": NERF_F16X3}
@@ -374,6 +375,11 @@ class Device:
         for the rendered pass and (``coarse``) the hierarchical coarse pass's weights."""
         _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_FUSED_COMPOSITE,
                                             (1 if enable else 0) | (2 if enable and coarse else 0)))
+
+    def set_coarse_precision(self, precision: Optional[int]) -> None:
+        """NERF_OPT_COARSE_PRECISION: the hierarchical coarse pass's precision (None: the render's)."""
+        _check(self.lib.nerf_ctx_set_option(self._ctx, NERF_OPT_COARSE_PRECISION,
+                                            -1 if precision is None else int(precision)))
 
     def stage_ms_history(self, n: int) -> list:
         """Per-stage device ms of each of the last n renders (n <= 64), oldest first."""

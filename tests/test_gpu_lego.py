@@ -270,10 +270,10 @@ def test_lego_headline_full_frames_error_report(ckpt, golden, precision):
 
 
 def test_lego_fp8_vs_reference_compressed(ckpt, golden):
-    """Config 5's bar on Lego: the fp8 path at least as close to the reference's fp32 render as
-    the reference's own int8 compressed renderer (src/benchmark/compressed_renderer.py, rendered
-    by it: compressed_lego.npz), in max AND mean RGB, on suite view 0 and the off-axis pose
-    (200x150x32).  Round 5's kernel keeps L0, L1, C0, the heads and the encodings on the bf16
+    """Config 5's bar on Lego at 200x150x32: the fp8 path at least as close to the reference's
+    fp32 render as the reference's own int8 compressed renderer (src/benchmark/compressed_renderer.py,
+    rendered by it: compressed_lego.npz), in max AND mean RGB, on suite view 0 and the off-axis
+    pose (the whole 800x600x128 frames: the test below).  Round 5's kernel keeps L0, L1, C0, the heads and the encodings on the bf16
     MFMA (tools/fp8_mixed_lab.py; the all-fp8 network of rounds 1-4 was 1.9x further off in max)."""
     g, gc = golden("render_lego_200x150_s32"), golden("compressed_lego")
     r = renderer(ckpt, "fp8")
@@ -285,5 +285,30 @@ def test_lego_fp8_vs_reference_compressed(ckpt, golden):
         print(f"lego 200x150x32 view {int(g['pose_ids'][kg])} vs the reference's fp32 render: fp8 rgb max {e8.max():.3e} "
               f"mean {e8.mean():.3e}; reference int8 compressed rgb max {ec.max():.3e} mean {ec.mean():.3e}; "
               f"fp8 closer in max: {bool(e8.max() < ec.max())}, in mean: {bool(e8.mean() < ec.mean())}")
+        assert np.isfinite(e8).all()
+        assert e8.max() < ec.max() and e8.mean() < ec.mean()
+
+
+def test_lego_fp8_vs_reference_compressed_full_frames(ckpt, golden):
+    """Config 5's bar at config 5's own size: on whole 800x600x128 frames of
+    suite view 0 and the off-axis pose, the fp8 path is closer to the reference's fp32 render
+    (render_lego_800x600_s128_full.npz) than the reference's own int8 CompressedNeRFRenderer
+    (compressed_lego_800x600_s128.npz, rendered by it through its own pieces in 4096-ray chunks,
+    make_golden_compressed.py --lego-full; compressed_renderer.py:161-211, 233-269, 311-358), in
+    max AND mean RGB."""
+    g, gc = golden(FULL), golden("compressed_lego_800x600_s128")
+    r = renderer(ckpt, "fp8")
+    for kc, pid in enumerate(gc["pose_ids"]):
+        kg = int(np.flatnonzero(g["pose_ids"] == pid)[0])
+        assert np.array_equal(gc["poses"][kc], g["poses"][kg])
+        rgb, depth = r.render_image(torch.from_numpy(g["poses"][kg]), (800, 600), 128)
+        e8 = np.abs(rgb.cpu().numpy() - g[f"rgb_{kg}"])
+        ec = np.abs(gc[f"rgb_{kc}"] - g[f"rgb_{kg}"])
+        d8 = np.abs(depth.cpu().numpy() - g[f"depth_{kg}"])
+        dc = np.abs(gc[f"depth_{kc}"] - g[f"depth_{kg}"])
+        print(f"lego 800x600x128 view {int(pid)} vs the reference's fp32 render: fp8 rgb max {e8.max():.3e} mean "
+              f"{e8.mean():.3e}, depth > 1e-2 on {int((d8 > 1e-2).sum())}; reference int8 compressed rgb max "
+              f"{ec.max():.3e} mean {ec.mean():.3e}, depth > 1e-2 on {int((dc > 1e-2).sum())}; fp8 closer in max: "
+              f"{bool(e8.max() < ec.max())}, in mean: {bool(e8.mean() < ec.mean())}")
         assert np.isfinite(e8).all()
         assert e8.max() < ec.max() and e8.mean() < ec.mean()
