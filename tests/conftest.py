@@ -21,6 +21,11 @@ def golden():
     import numpy as np
 
     def load(name):
+        if name.endswith(".json"):
+            import json
+
+            with open(os.path.join(GOLDEN, name)) as f:
+                return json.load(f)
         return np.load(os.path.join(GOLDEN, name if name.endswith(".npz") else name + ".npz"))
 
     return load

@@ -23,10 +23,10 @@ tell which rays the GPU rendered on the very samples the reference chain used.
         bounded at 1.5x their round-5 measurement;
   (iv)  the truth: the same chain in float64 (render_lego_800x600_c3_fp64.npz,
         ``make_golden.py --lego-c3-fp64``).  The hierarchical chain is ill-conditioned at a few
-        hundred rays per frame (a last-bit change of a coarse weight moves a fine sample), so
+        thousand rays per frame (a last-bit change of a coarse weight moves a fine sample), so
         no fp32 implementation can match another one there; what is asserted is that the GPU's
-        fp32 and f16x3 renders are no further from the float64 truth than the reference's own
-        fp32 chain is -- in pixels over 1e-4 and in max RGB / depth error.
+        fp32 render (and f16x3 with an fp32 coarse pass) is no further from the float64 truth
+        than two fp32 CPU implementations of the chain are (c3_truth_spread.json).
 """
 import os
 
@@ -158,24 +158,47 @@ def truth_stats(rgb, depth, t_rgb, t_dep):
             "over": int(((e_rgb >= TOL) | (e_dep >= TOL)).sum())}
 
 
+def fp32_envelope(spread, pose_id, ref):
+    """The worse of two fp32 CPU implementations of the chain against the float64 truth: the
+    reference's own pieces (the fixture) and the oracle's restatement run on a GPU box's host CPU,
+    whose GEMM kernels sum in another order (tests/golden/c3_truth_spread.json)."""
+    o = next(v for v in spread["views"] if v["pose_id"] == pose_id)["oracle_fp32_chain"]
+    return {"over": max(ref["over"], o["over_1e-4"]), "rgb_max": max(ref["rgb_max"], o["rgb_max"]),
+            "rgb_mean": max(ref["rgb_mean"], o["rgb_mean"]), "depth_max": max(ref["depth_max"], o["depth_max"])}
+
+
 @pytest.mark.parametrize("precision,coarse", [("fp32", None), ("f16x3", "fp32"), ("f16x3", None)])
 def test_lego_c3_no_further_from_fp64_than_reference(ckpt, golden, precision, coarse):
     """(iv) against the float64 run of the same chain (rendering.py:72-143 with the gather fixed,
-    base_renderer.py:165-281, nerf.py:92-131 in float64), per view: pixels over 1e-4, max and mean
-    RGB and max depth error of the GPU render beside the reference's own fp32 chain's
-    (render_lego_800x600_c3_full.npz).  PENDING: bounds set from the round-6 measurement."""
-    g, t = golden(C3), golden(C3_FP64)
+    base_renderer.py:165-281, nerf.py:92-131 in float64).  Two fp32 CPU implementations -- the
+    reference's own pieces and the oracle on another host CPU -- are 3,432-3,450 (view 0) and
+    5,660-5,690 (off-axis) pixels over 1e-4 from it, with RGB max 5.7e-3-8.9e-3: in this chain a
+    last-bit change of a coarse weight moves fine samples, so no fp32 implementation is closer.
+    The GPU's fp32 path, and f16x3 with its coarse pass in fp32 (NERF_OPT_COARSE_PRECISION),
+    have no more pixels over 1e-4 than the worse of the two CPU implementations, a mean error
+    within 5 % of it, and max RGB / depth errors (single-pixel statistics) within 25 % of its.
+    f16x3 with its own split-fp16 coarse pass (2^-22 operands against fp32's 2^-24) is further:
+    its count stays within 5 % of the envelope and its mean within 10 % (the max is reported)."""
+    g, t, spread = golden(C3), golden(C3_FP64), golden("c3_truth_spread.json")
     w, h = int(g["W"]), int(g["H"])
     r = renderer(ckpt, precision, coarse)
     for k in range(len(g["pose_ids"])):
         assert np.array_equal(g["poses"][k], t["poses"][k])
         rgb, depth = r.render_image(torch.from_numpy(g["poses"][k]), (w, h), NC)
         ref = truth_stats(g[f"rgb_{k}"], g[f"depth_{k}"], t[f"rgb_{k}"], t[f"depth_{k}"])
+        env = fp32_envelope(spread, int(g["pose_ids"][k]), ref)
         gpu = truth_stats(rgb.cpu().numpy(), depth.cpu().numpy(), t[f"rgb_{k}"], t[f"depth_{k}"])
         print(f"lego C3 view {int(g['pose_ids'][k])} vs float64: reference fp32 chain rgb max {ref['rgb_max']:.3e} "
-              f"mean {ref['rgb_mean']:.3e} depth max {ref['depth_max']:.3e} over {TOL}: {ref['over']}; GPU {precision}"
+              f"mean {ref['rgb_mean']:.3e} depth max {ref['depth_max']:.3e} over {TOL}: {ref['over']}; fp32 CPU "
+              f"envelope rgb max {env['rgb_max']:.3e} over {env['over']}; GPU {precision}"
               f"{'' if coarse is None else ' (' + coarse + ' coarse)'} rgb max {gpu['rgb_max']:.3e} mean "
               f"{gpu['rgb_mean']:.3e} depth max {gpu['depth_max']:.3e} over: {gpu['over']}")
+        if precision == "fp32" or coarse == "fp32":
+            assert gpu["over"] <= env["over"]
+            assert gpu["rgb_mean"] <= 1.05 * env["rgb_mean"]
+            assert gpu["rgb_max"] <= 1.25 * env["rgb_max"] and gpu["depth_max"] <= 1.25 * env["depth_max"]
+        else:
+            assert gpu["over"] <= 1.05 * env["over"] and gpu["rgb_mean"] <= 1.10 * env["rgb_mean"]
 
 
 # Per view (suite 0, off-axis): RGB max, RGB mean and pixels with depth moved by > 1e-2 against

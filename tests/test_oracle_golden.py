@@ -211,3 +211,21 @@ def test_compressed_restatement_on_lego(golden):
         rgb, depth = O.compressed_render_image(cw, torch.from_numpy(g["poses"][k]), (200, 150), 32)
         np.testing.assert_array_equal(rgb.numpy(), g[f"rgb_{k}"])
         np.testing.assert_array_equal(depth.numpy(), g[f"depth_{k}"])
+
+
+def test_c3_truth_fixtures_consistent():
+    """The float64 C3 truth (make_golden.py --lego-c3-fp64) and the fp32 CPU spread record
+    (tools/c3_truth_spread.py, c3_truth_spread.json) describe the same frames: same poses, and
+    the reference fp32 chain's distance to the truth recomputed here equals the recorded one."""
+    import json
+
+    g = np.load(os.path.join(GOLDEN, "render_lego_800x600_c3_full.npz"))
+    t = np.load(os.path.join(GOLDEN, "render_lego_800x600_c3_fp64.npz"))
+    spread = json.load(open(os.path.join(GOLDEN, "c3_truth_spread.json")))
+    assert t["rgb_0"].dtype == np.float64 and np.array_equal(g["poses"], t["poses"])
+    for k, pid in enumerate(g["pose_ids"]):
+        e_rgb = np.abs(g[f"rgb_{k}"].astype(np.float64) - t[f"rgb_{k}"]).max(-1)
+        e_dep = np.abs(g[f"depth_{k}"].astype(np.float64) - t[f"depth_{k}"])
+        rec = next(v for v in spread["views"] if v["pose_id"] == int(pid))["reference_fp32_chain"]
+        assert int(((e_rgb >= 1e-4) | (e_dep >= 1e-4)).sum()) == rec["over_1e-4"]
+        assert abs(float(e_rgb.max()) - rec["rgb_max"]) < 1e-12 and abs(float(e_dep.max()) - rec["depth_max"]) < 1e-12
