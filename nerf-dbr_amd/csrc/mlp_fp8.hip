@@ -168,18 +168,27 @@ struct Ctx {
 // stream is not restaged after the ring's first fill; NOBARRIER -- no seam barriers; NOREAD --
 // the ring's first fragments reused; NOCONV -- accumulator bits as the next layer's operands;
 // PE_ONCE -- the first tile's encodings reused.
-__device__ __forceinline__ void stage_chunk(const Ctx& cx, int c) {
+__device__ __forceinline__ void stage_piece(const Ctx& cx, int c, int i) {
 #ifdef NERF_FP8_ABLATE_NODMA
   if (c >= kSlots) return;
 #endif
   const int slot = (c + cx.rot) & (kSlots - 1);
   const unsigned dst = cx.lds_base + unsigned(kLdsRingOff + slot * kChunkB + cx.wave_u * 1024);
   const int src = c < kTotalChunks ? c : c - kTotalChunks;
-#pragma unroll
-  for (int i = 0; i < kGldsPerStage; ++i)
-    lds_dma_16_s(cx.blob + size_t(src) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
-                 dst + unsigned(i * kThreads * 16));
+  lds_dma_16_s(cx.blob + size_t(src) * kChunkB, unsigned(cx.wave_u * 1024 + cx.lane * 16 + i * kThreads * 16),
+               dst + unsigned(i * kThreads * 16));
 }
+__device__ __forceinline__ void stage_chunk(const Ctx& cx, int c) {
+#pragma unroll
+  for (int i = 0; i < kGldsPerStage; ++i) stage_piece(cx, c, i);
+}
+// NERF_FP8_SPREAD (with NERF_FP8_AHEAD=2): a seam stages the first LDS-DMA piece of its chunk and
+// the next units one piece each, instead of all of the wave's pieces back to back at the seam.
+#ifndef NERF_FP8_SPREAD
+#define NERF_FP8_SPREAD 0
+#endif
+static_assert(!NERF_FP8_SPREAD || (kAhead == 2 && kGldsPerStage <= kChunkUnits),
+              "spread pieces land within the chunk after the next seam");
 
 // Seam before this wave's first read of the tile's chunk c: its own pieces of c landed
 // (nothing younger is in flight: vmcnt(0)), the barrier publishes c to every wave and frees
@@ -193,11 +202,21 @@ __device__ __forceinline__ void seam(const Ctx& cx, int c) {
   __builtin_amdgcn_s_barrier();
 #endif
   compiler_fence();
-  stage_chunk(cx, c + kAhead + cx.lag);
+  if (NERF_FP8_SPREAD) stage_piece(cx, c + kAhead, 0);
+  else stage_chunk(cx, c + kAhead + cx.lag);
 }
 // The seam inside the unit sequence: before unit body n when its prefetch (unit n + kPf)
 // is the first unit of a chunk.
+NL_HD bool seam_unit(int m) { return m >= 0 && (m + kPf) % kChunkUnits == 0 && m + kPf < kUnits; }
 __device__ __forceinline__ void seam_before(const Ctx& cx, int n) {
+  if (NERF_FP8_SPREAD) {   // the pieces 1.. of the chunk the seam i units back staged (-1: the tile top)
+#pragma unroll
+    for (int i = 1; i < kGldsPerStage; ++i) {
+      const int m = n - i;
+      if (m == -1) stage_piece(cx, kAhead, i);
+      else if (seam_unit(m)) stage_piece(cx, (m + kPf) / kChunkUnits + kAhead, i);
+    }
+  }
   if ((n + kPf) % kChunkUnits != 0 || n + kPf >= kUnits) return;
   seam(cx, (n + kPf) / kChunkUnits);
 }
@@ -542,7 +561,8 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
       wait_vmcnt(kGldsPerStage);                     // own pieces of chunk 0 (chunk 1 may be in flight)
       __syncthreads();
       if (cx.lag) seam(cx, 0);
-      if (kAhead == 2) stage_chunk(cx, 2);           // what the tile-top seam stages on later tiles
+      if (kAhead == 2 && NERF_FP8_SPREAD) stage_piece(cx, 2, 0);   // what the tile-top seam stages later
+      else if (kAhead == 2) stage_chunk(cx, 2);
     } else {
       seam(cx, 0);
 #pragma unroll
