@@ -48,7 +48,8 @@ enum nerf_precision {
                     compressed-weights path (config 5; the reference's int8
                     CompressedNeRFRenderer, src/benchmark/compressed_renderer.py, is its error
                     bar: on the Lego checkpoint this path is the closer of the two to the fp32
-                    render, in max and mean RGB) */
+                    render, in max and mean RGB, at 200x150x32 and on whole 800x600x128 frames
+                    of suite view 0 and an off-axis pose) */
   NERF_BF16X3 = 3, /* split bf16 on the bf16 MFMA: W.X ~ Wh.Xh + Wh.Xl + Wl.Xh with
                       v = vh + vl, vh = bf16(v), vl = bf16(v - vh); f32 accumulate,
                       accurate encodings: a parity-grade fast path (RGB/depth
