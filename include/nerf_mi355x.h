@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NERF_ABI_VERSION 5
+#define NERF_ABI_VERSION 6
 
 enum nerf_status {
   NERF_OK = 0,
@@ -86,12 +86,31 @@ int nerf_device_name(int device, char* buf, int buf_len);
  * be freed after the call returns. */
 int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, int n_params);
 
+/* Network layouts ("optionally a second original-NeRF weight-layout loader").
+ *   NERF_LAYOUT_NERFMODEL: the reference's NeRFModel (src/models/nerf.py:48-131), as above.
+ *   NERF_LAYOUT_ORIGINAL_NERF: the original NeRF implementation's network, as the reference's
+ *   bundled Lego weights hold it (data/lego_example_weights, args.txt: 8x256, multires 10 / 4):
+ *   position encoding re-entering at layer 5 (cat([pe, h]) there), encodings sin(2^k x) without
+ *   pi, view directions normalised before their encoding, a linear feature layer before the
+ *   views layer.  The 22 tensors are passed in NeRFModel's order and [out, in] orientation with
+ *   three changes the host makes (nerf_amd/weights.py original_nerf_tensors): layers.4 is
+ *   [256, 256], layers.5 is [256, 319] with its columns re-ordered to [h, pe], and
+ *   color_layers.0 is the views layer with the feature layer folded in (W_v[:, :256] W_f,
+ *   bias W_v[:, :256] b_f + b_v, in float64).  Rendered on NERF_FP32 only (other precisions are
+ *   refused for such a net). */
+#define NERF_LAYOUT_NERFMODEL 0
+#define NERF_LAYOUT_ORIGINAL_NERF 1
+int nerf_ctx_load_weights_layout(nerf_ctx* ctx, int net, int layout, const float* const* params, int n_params);
+
 /* Pure host helper (no device needed): packs one network into the three blobs
  * the kernels read.  Sizes in bytes via nerf_packed_sizes.  Used by the
  * loader above and by host-side layout tests. */
 void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob);
 int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob, uint16_t* bf16_blob,
                       float* param_blob);
+/* The f32 and params blobs of a network in either layout (NERF_LAYOUT_*). */
+int nerf_pack_weights_layout(const float* const* params, int n_params, int layout, float* f32_blob,
+                             float* param_blob);
 
 /* Pure host helpers for the fp8 path: the packed mixed blob the fp8 kernel reads (the fp8
  * layers' e4m3 fragment units, the bf16 units of L0, L1, C0, L4's encoding inputs and the

@@ -51,6 +51,7 @@ struct NetDev {
   bool f16x3_ok = false;    // the loaded weights fit fp16's range
   float* params = nullptr;
   bool loaded = false;
+  int layout = NERF_LAYOUT_NERFMODEL;   // NERF_LAYOUT_ORIGINAL_NERF: f32 blob + params only
 };
 
 struct nerf_ctx {
@@ -117,6 +118,8 @@ int check_net(nerf_ctx* ctx, int net, int precision) {
       precision != NERF_F16X3)
     return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (!ctx->net[net].loaded) return set_error(NERF_E_NO_WEIGHTS, "%s network not loaded", net ? "fine" : "coarse");
+  if (ctx->net[net].layout == NERF_LAYOUT_ORIGINAL_NERF && precision != NERF_FP32)
+    return set_error(NERF_E_INVALID, "%s network has the original-NeRF layout: NERF_FP32 only", net ? "fine" : "coarse");
   if (precision == NERF_F16X3 && !ctx->net[net].f16x3_ok)
     return set_error(NERF_E_INVALID, "%s network has weights outside fp16's range: NERF_F16X3 unavailable",
                      net ? "fine" : "coarse");
@@ -141,7 +144,7 @@ hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, 
   if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_BF16X3) return launch_mlp_bf16x3(nd.bf16x3, nd.params, src, n, out, expl, s, seg);
   if (precision == NERF_F16X3) return launch_mlp_f16x3(nd.f16x3, nd.params, src, n, out, expl, s, seg, ctx->d_range);
-  return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s);
+  return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s, nd.layout);
 }
 
 }  // namespace
@@ -246,6 +249,29 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
   HIP_TRY(hipMemcpy(nd.bf16, bf.data(), nbf16, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));
   nd.loaded = true;
+  nd.layout = NERF_LAYOUT_NERFMODEL;
+  return NERF_OK;
+}
+
+int nerf_ctx_load_weights_layout(nerf_ctx* ctx, int net, int layout, const float* const* params, int n_params) {
+  if (layout == NERF_LAYOUT_NERFMODEL) return nerf_ctx_load_weights(ctx, net, params, n_params);
+  if (!ctx) return set_error(NERF_E_INVALID, "null context");
+  if (net != NERF_NET_COARSE && net != NERF_NET_FINE) return set_error(NERF_E_INVALID, "bad net %d", net);
+  if (layout != NERF_LAYOUT_ORIGINAL_NERF) return set_error(NERF_E_INVALID, "unknown layout %d", layout);
+  size_t nf32, nbf16, nprm;
+  nerf_packed_sizes(&nf32, &nbf16, &nprm);
+  std::vector<float> f32(nf32 / 4), prm(nprm / 4);
+  int rc = nerf_pack_weights_layout(params, n_params, layout, f32.data(), prm.data());
+  if (rc != NERF_OK) return rc;
+  DeviceGuard g(ctx->device);
+  NetDev& nd = ctx->net[net];
+  if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
+  if (!nd.params) HIP_TRY(hipMalloc((void**)&nd.params, nprm));
+  HIP_TRY(hipMemcpy(nd.f32, f32.data(), nf32, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));
+  nd.f16x3_ok = false;   // the other precisions' blobs (if any) belong to an earlier network
+  nd.loaded = true;
+  nd.layout = layout;
   return NERF_OK;
 }
 

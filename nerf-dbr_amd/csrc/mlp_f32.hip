@@ -20,24 +20,25 @@ namespace {
 
 constexpr int kWavesF32 = 4;
 
-template <int L>
+template <int L, int kSkip>
 constexpr int f32_layer_offset() {   // in floats
   int off = 0;
-  for (int l = 0; l < L; ++l) off += f32_layer_floats(l);
+  for (int l = 0; l < L; ++l) off += f32_layer_floats(l, kSkip);
   return off;
 }
 
-// One MFMA layer: acc[0..NT) = bias + W . [prev | ext]
-template <int L, int NT, int NEXT>
+// One MFMA layer: acc[0..NT) = bias + W . [prev | ext]; kSkip: the layer that takes the
+// position encoding again (nerf_layout.h)
+template <int L, int NT, int NEXT, int kSkip>
 __device__ __forceinline__ void layer_f32(f32x16 (&acc)[8], const f32x16 (&prev)[8], const float (&ext)[NEXT],
                                           const f32x4* __restrict__ blob, const float* __restrict__ prm,
                                           int lane, int h) {
-  constexpr LayerShape sh = layer_shape(L);
+  constexpr LayerShape sh = layer_shape(L, kSkip);
   constexpr int KH = sh.hidden / 2;         // hidden k-steps
-  constexpr int KU = ksteps_f32(L);
+  constexpr int KU = ksteps_f32(L, kSkip);
   static_assert(KU == KH + (sh.extra == kNone ? 0 : NEXT), "layer/ext mismatch");
   load_bias<NT>(acc, prm, L, h);
-  const f32x4* a_base = blob + f32_layer_offset<L>() / 4 + lane;
+  const f32x4* a_base = blob + f32_layer_offset<L, kSkip>() / 4 + lane;
 #pragma unroll
   for (int ug = 0; ug < KU / 4; ++ug) {
     f32x4 a[NT];
@@ -55,7 +56,11 @@ __device__ __forceinline__ void layer_f32(f32x16 (&acc)[8], const f32x16 (&prev)
   }
 }
 
-template <bool kExplicit>
+// kOrig: the original NeRF implementation's network (nerf_ctx_load_weights_layout, layout 1):
+// the position encoding re-enters at layer 5, the encodings have no pi, and the view
+// directions are normalised before their encoding; its feature layer (linear, no activation)
+// arrives folded into C0 by the host.  Otherwise NeRFModel (nerf.py:92-131).
+template <bool kExplicit, bool kOrig = false>
 __global__ __launch_bounds__(256, 1) void mlp_f32_kernel(const f32x4* __restrict__ blob,
                                                          const float* __restrict__ prm, SampleSrc src,
                                                          long n_points, f32x4* __restrict__ out) {
@@ -69,28 +74,34 @@ __global__ __launch_bounds__(256, 1) void mlp_f32_kernel(const f32x4* __restrict
   float x[3], d[3];
   fetch_sample<kExplicit>(src, pc, x, d);
   float pe[32], de[16];
-  pos_encode(x[0], x[1], x[2], h, pe);
-  dir_encode(d[0], d[1], d[2], h, de);
+  constexpr int S = kOrig ? kSkipOriginal : kSkipNeRFModel;
+  pos_encode<false, false, kOrig>(x[0], x[1], x[2], h, pe);
+  if (kOrig) {   // the original's viewdirs = rays_d / |rays_d| (its encoding input)
+    const float n = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d[0], d[0]), __fmul_rn(d[1], d[1])), __fmul_rn(d[2], d[2])));
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = __fdiv_rn(d[c], n);
+  }
+  dir_encode<false, false, kOrig>(d[0], d[1], d[2], h, de);
 
   f32x16 a[8], b[8];
-  layer_f32<L0, 8, 32>(a, b, pe, blob, prm, lane, h);   // b unused (no hidden input)
+  layer_f32<L0, 8, 32, S>(a, b, pe, blob, prm, lane, h);   // b unused (no hidden input)
   relu_tiles<8>(a);
-  layer_f32<L1, 8, 32>(b, a, pe, blob, prm, lane, h);
+  layer_f32<L1, 8, 32, S>(b, a, pe, blob, prm, lane, h);
   relu_tiles<8>(b);
-  layer_f32<L2, 8, 32>(a, b, pe, blob, prm, lane, h);
+  layer_f32<L2, 8, 32, S>(a, b, pe, blob, prm, lane, h);
   relu_tiles<8>(a);
-  layer_f32<L3, 8, 32>(b, a, pe, blob, prm, lane, h);
+  layer_f32<L3, 8, 32, S>(b, a, pe, blob, prm, lane, h);
   relu_tiles<8>(b);
-  layer_f32<L4, 8, 32>(a, b, pe, blob, prm, lane, h);   // skip: [x, pe] (nerf.py:109-110)
+  layer_f32<L4, 8, 32, S>(a, b, pe, blob, prm, lane, h);   // NeRFModel's skip: [x, pe] (nerf.py:109-110)
   relu_tiles<8>(a);
-  layer_f32<L5, 8, 32>(b, a, pe, blob, prm, lane, h);
+  layer_f32<L5, 8, 32, S>(b, a, pe, blob, prm, lane, h);   // the original's skip ([pe, h], re-ordered)
   relu_tiles<8>(b);
-  layer_f32<L6, 8, 32>(a, b, pe, blob, prm, lane, h);
+  layer_f32<L6, 8, 32, S>(a, b, pe, blob, prm, lane, h);
   relu_tiles<8>(a);
-  layer_f32<L7, 8, 32>(b, a, pe, blob, prm, lane, h);
+  layer_f32<L7, 8, 32, S>(b, a, pe, blob, prm, lane, h);
   relu_tiles<8>(b);
   const float sigma = density_head(b, prm, h);
-  layer_f32<C0, 4, 16>(a, b, de, blob, prm, lane, h);   // [x, PE4(d)] (nerf.py:117-121)
+  layer_f32<C0, 4, 16, S>(a, b, de, blob, prm, lane, h);   // [x, PE4(d)] (nerf.py:117-121)
   relu_tiles<4>(a);
   float rgb[3];
   color_head(a, prm, h, rgb);
@@ -100,15 +111,22 @@ __global__ __launch_bounds__(256, 1) void mlp_f32_kernel(const f32x4* __restrict
 }  // namespace
 
 hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSrc& src, long n_points,
-                          float* out, bool explicit_points, hipStream_t stream) {
+                          float* out, bool explicit_points, hipStream_t stream, int layout) {
   if (n_points <= 0) return hipSuccess;
   const long per_block = long(kWavesF32) * kSamplesPerWave;
   const long blocks = (n_points + per_block - 1) / per_block;
   if (blocks > 0x7FFFFFFFL) return hipErrorInvalidValue;
   const dim3 grid{unsigned(blocks), 1, 1}, block{64 * kWavesF32, 1, 1};
-  if (explicit_points)
+  if (layout != 0 && layout != 1) return hipErrorInvalidValue;
+  if (explicit_points && layout == 1)
+    hipLaunchKernelGGL((mlp_f32_kernel<true, true>), grid, block, 0, stream, (const f32x4*)blob, params, src, n_points,
+                       (f32x4*)out);
+  else if (explicit_points)
     hipLaunchKernelGGL(mlp_f32_kernel<true>, grid, block, 0, stream, (const f32x4*)blob, params, src, n_points,
                        (f32x4*)out);
+  else if (layout == 1)
+    hipLaunchKernelGGL((mlp_f32_kernel<false, true>), grid, block, 0, stream, (const f32x4*)blob, params, src,
+                       n_points, (f32x4*)out);
   else
     hipLaunchKernelGGL(mlp_f32_kernel<false>, grid, block, 0, stream, (const f32x4*)blob, params, src, n_points,
                        (f32x4*)out);

@@ -92,8 +92,13 @@ __device__ __forceinline__ void sincos_doubling(float c0, float x, float* s, flo
   }
 }
 
-template <bool kFast = false, bool kOcml = false>
+// kNoPi: the original NeRF implementation's encoding sin(2^k x), cos(2^k x) (no pi; the
+// teacher layout of SURVEY §8f row 1), accurate path only.
+__device__ __forceinline__ float enc_coef(int k, bool no_pi) { return no_pi ? __builtin_ldexpf(1.0f, k) : pe_coef(k); }
+
+template <bool kFast = false, bool kOcml = false, bool kNoPi = false>
 __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, float (&pe)[32]) {
+  static_assert(!(kFast && kNoPi), "the no-pi encoding has the accurate path only");
   const float xs[3] = {x0, x1, x2};
   if (kFast) {
 #pragma unroll
@@ -109,7 +114,7 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
   } else {
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk) {
-      const float c = pe_coef(5 * h + kk);
+      const float c = enc_coef(5 * h + kk, kNoPi);
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
         float s, co;
@@ -123,8 +128,9 @@ __device__ __forceinline__ void pos_encode(float x0, float x1, float x2, int h, 
   pe[31] = h ? 0.0f : x1;
 }
 
-template <bool kFast = false, bool kOcml = false>
+template <bool kFast = false, bool kOcml = false, bool kNoPi = false>
 __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, float (&de)[16]) {
+  static_assert(!(kFast && kNoPi), "the no-pi encoding has the accurate path only");
   const float ds[3] = {d0, d1, d2};
   if (kFast) {
 #pragma unroll
@@ -140,7 +146,7 @@ __device__ __forceinline__ void dir_encode(float d0, float d1, float d2, int h, 
   } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const float c = pe_coef(2 * h + kk);
+      const float c = enc_coef(2 * h + kk, kNoPi);
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
         float s, co;

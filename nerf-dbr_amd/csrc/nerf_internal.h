@@ -24,8 +24,10 @@ int current_device_cus();
 
 hipError_t launch_generate_rays(const float* c2w_rowmajor16, int width, int height, int row0, int row1,
                                 float focal, float* rays_o, float* rays_d, hipStream_t stream);
+// layout: 0 = NeRFModel (nerf.py), 1 = the original NeRF implementation's trunk (skip into
+// layer 5, encodings without pi, normalised view directions; nerf_ctx_load_weights_layout)
 hipError_t launch_mlp_f32(const float* blob, const float* params, const SampleSrc& src, long n_points,
-                          float* out, bool explicit_points, hipStream_t stream);
+                          float* out, bool explicit_points, hipStream_t stream, int layout = 0);
 // seg (render passes with n_samples % 32 == 0 only): compositing fused into the
 // epilogue, one 32-B SegRecord per 32-sample segment instead of out's (sigma, rgb);
 // wloc (with seg): each sample's in-segment weight as well (hierarchical coarse pass)

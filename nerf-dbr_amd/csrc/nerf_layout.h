@@ -70,21 +70,30 @@ struct LayerShape {
   int extra;      // Extra kind appended after the hidden inputs
 };
 
-NL_HD LayerShape layer_shape(int l) {
+// The trunk layer whose input carries the position encoding again: NeRFModel's skip feeds
+// layers[4] with cat([x, pe]) (nerf.py:109-110); the original NeRF implementation's feeds its
+// layer 5 with cat([pe, h]) (data/lego_example_weights, args.txt), which the
+// host re-orders to [h, pe] so that one k map serves both (nerf_amd/weights.py).
+constexpr int kSkipNeRFModel = L4, kSkipOriginal = L5;
+
+NL_HD LayerShape layer_shape(int l, int skip = kSkipNeRFModel) {
   if (l == L0) return {kHidden, kPosDim, 0, kPos};
-  if (l == L4) return {kHidden, kHidden + kPosDim, kHidden, kPos};
+  if (l == skip) return {kHidden, kHidden + kPosDim, kHidden, kPos};
   if (l == C0) return {kColorHidden, kHidden + kDirDim, kHidden, kDir};
   return {kHidden, kHidden, kHidden, kNone};
 }
 NL_HD int extra_slots(int kind) { return kind == kPos ? 32 : kind == kDir ? 16 : 0; }
 NL_HD int out_tiles(int l) { return layer_shape(l).out / 32; }
-NL_HD int ksteps_f32(int l) { LayerShape s = layer_shape(l); return s.hidden / 2 + extra_slots(s.extra); }
+NL_HD int ksteps_f32(int l, int skip = kSkipNeRFModel) {
+  LayerShape s = layer_shape(l, skip);
+  return s.hidden / 2 + extra_slots(s.extra);
+}
 NL_HD int ksteps_bf16(int l) { LayerShape s = layer_shape(l); return s.hidden / 16 + extra_slots(s.extra) / 8; }
 
 // Reference column index of the weight that multiplies the value lane half h
 // supplies at (k-step u, element j) -- or -1 for padding.
-NL_HD int f32_k_col(int l, int u, int h) {
-  LayerShape s = layer_shape(l);
+NL_HD int f32_k_col(int l, int u, int h, int skip = kSkipNeRFModel) {
+  LayerShape s = layer_shape(l, skip);
   int nh = s.hidden / 2;
   if (u < nh) return hid_f32_feature(u, h);
   int q = u - nh;
@@ -125,7 +134,7 @@ constexpr int kParamFloats = kC1B + 4;              // 2952
 constexpr int kUnitBytes = 2048;                    // one k-step of one quarter
 constexpr int kUnitsPerChunk = kChunkBytes / kUnitBytes;
 
-NL_HD int f32_layer_floats(int l) { return ksteps_f32(l) * out_tiles(l) * 64; }
+NL_HD int f32_layer_floats(int l, int skip = kSkipNeRFModel) { return ksteps_f32(l, skip) * out_tiles(l) * 64; }
 NL_HD int bf16_layer_units(int l) { return (out_tiles(l) / 2) * ksteps_bf16(l); }
 NL_HD int bf16_unit_base(int l) {                   // first unit of layer l
   int n = 0;

@@ -19,6 +19,8 @@ constexpr int kSpecOfLayer[kNumMfmaLayers] = {0, 1, 2, 3, 4, 5, 6, 7, 9};
 constexpr int kSpecDensity = 8, kSpecColor1 = 10;
 constexpr int kSpecOut[11] = {256, 256, 256, 256, 256, 256, 256, 256, 1, 128, 3};
 constexpr int kSpecIn[11] = {63, 256, 256, 256, 319, 256, 256, 256, 256, 283, 128};
+// the original NeRF implementation's trunk (NERF_LAYOUT_ORIGINAL_NERF): the skip input on layer 5
+constexpr int kSpecInOrig[11] = {63, 256, 256, 256, 256, 319, 256, 256, 256, 283, 128};
 
 uint16_t f32_to_bf16_rne(float f) {
   uint32_t u;
@@ -214,6 +216,41 @@ extern "C" void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* p
   if (param_blob) *param_blob = size_t(kParamFloats) * sizeof(float);
 }
 
+namespace {
+
+// f32 A blob (nerf_layout.h) and the params blob of either network layout
+void pack_f32(const float* const* params, int skip, float* f32_blob) {
+  const int* in = skip == kSkipOriginal ? kSpecInOrig : kSpecIn;
+  auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * in[spec] + k]; };
+  float* dst = f32_blob;
+  for (int l = 0; l < kNumMfmaLayers; ++l) {
+    const int spec = kSpecOfLayer[l], nt = out_tiles(l), ku = ksteps_f32(l, skip);
+    for (int ug = 0; ug < ku / 4; ++ug)
+      for (int o = 0; o < nt; ++o)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int i = 0; i < 4; ++i) {
+            const int col = f32_k_col(l, 4 * ug + i, lane >> 5, skip);
+            *dst++ = col < 0 ? 0.0f : W(spec, 32 * o + (lane & 31), col);
+          }
+  }
+}
+
+}  // namespace
+
+extern "C" int nerf_pack_weights_layout(const float* const* params, int n_params, int layout, float* f32_blob,
+                                        float* param_blob) {
+  if (layout != NERF_LAYOUT_NERFMODEL && layout != NERF_LAYOUT_ORIGINAL_NERF)
+    return set_error(NERF_E_INVALID, "nerf_pack_weights_layout: unknown layout %d", layout);
+  if (layout == NERF_LAYOUT_NERFMODEL) return nerf_pack_weights(params, n_params, f32_blob, nullptr, param_blob);
+  if (!params || n_params != NERF_N_PARAMS)
+    return set_error(NERF_E_INVALID, "nerf_pack_weights_layout: need %d tensors, got %d", NERF_N_PARAMS, n_params);
+  for (int i = 0; i < NERF_N_PARAMS; ++i)
+    if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_layout: tensor %d is NULL", i);
+  if (f32_blob) pack_f32(params, kSkipOriginal, f32_blob);
+  // the params blob reads only biases, the density head and colour-1: the same in both layouts
+  return param_blob ? nerf_pack_weights(params, n_params, nullptr, nullptr, param_blob) : NERF_OK;
+}
+
 extern "C" int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob,
                                  uint16_t* bf16_blob, float* param_blob) {
   if (!params || n_params != NERF_N_PARAMS) return set_error(NERF_E_INVALID, "nerf_pack_weights: need %d tensors, got %d", NERF_N_PARAMS, n_params);
@@ -222,19 +259,7 @@ extern "C" int nerf_pack_weights(const float* const* params, int n_params, float
   auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * kSpecIn[spec] + k]; };
   auto B = [&](int spec, int o) { return params[2 * spec + 1][o]; };
 
-  if (f32_blob) {
-    float* dst = f32_blob;
-    for (int l = 0; l < kNumMfmaLayers; ++l) {
-      const int spec = kSpecOfLayer[l], nt = out_tiles(l), ku = ksteps_f32(l);
-      for (int ug = 0; ug < ku / 4; ++ug)
-        for (int o = 0; o < nt; ++o)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int i = 0; i < 4; ++i) {
-              const int col = f32_k_col(l, 4 * ug + i, lane >> 5);
-              *dst++ = col < 0 ? 0.0f : W(spec, 32 * o + (lane & 31), col);
-            }
-    }
-  }
+  if (f32_blob) pack_f32(params, kSkipNeRFModel, f32_blob);
   if (bf16_blob) {
     std::vector<float> vals;
     bf16_stream_values(params, vals);

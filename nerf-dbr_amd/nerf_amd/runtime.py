@@ -30,6 +30,7 @@ NERF_N_PARAMS = 22
 NERF_N_STAGES = 5
 NERF_OPT_FUSED_COMPOSITE = 1
 NERF_OPT_COARSE_PRECISION = 2
+NERF_LAYOUT_NERFMODEL, NERF_LAYOUT_ORIGINAL_NERF = 0, 1
 STAGES = ("rays", "coarse_mlp", "importance", "fine_mlp", "composite")
 
 PRECISIONS = {"fp32": NERF_FP32, "bf16": NERF_BF16, "fp8": NERF_FP8, "bf16x3": NERF_BF16X3, "f16x3": NERF_F16X3}
@@ -45,6 +46,8 @@ SIGNATURES = {
     "nerf_ctx_destroy": (None, [_P]),
     "nerf_device_name": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_int]),
     "nerf_ctx_load_weights": (_c.c_int, [_P, _c.c_int, _c.POINTER(_FP), _c.c_int]),
+    "nerf_ctx_load_weights_layout": (_c.c_int, [_P, _c.c_int, _c.c_int, _c.POINTER(_FP), _c.c_int]),
+    "nerf_pack_weights_layout": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _c.c_int, _P, _P]),
     "nerf_packed_sizes": (None, [_c.POINTER(_c.c_size_t)] * 3),
     "nerf_pack_weights": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P, _P, _P]),
     "nerf_uniform_z": (None, [_FP, _c.c_int, _c.c_float, _c.c_float, _FP]),
@@ -182,6 +185,24 @@ def pack_weights(sd: Mapping[str, np.ndarray]):
     return f32, bf, prm
 
 
+def pack_weights_original_nerf(arrays):
+    """Host-only packing of the original NeRF implementation's 24 arrays
+    (NERF_LAYOUT_ORIGINAL_NERF, weights.original_nerf_tensors): (f32 blob, params)."""
+    from . import weights as W
+
+    lib = load_library()
+    sizes = [ctypes.c_size_t() for _ in range(3)]
+    lib.nerf_packed_sizes(*[ctypes.byref(s) for s in sizes])
+    f32 = np.zeros(sizes[0].value // 4, np.float32)
+    prm = np.zeros(sizes[2].value // 4, np.float32)
+    arrs = W.original_nerf_tensors(arrays)
+    ptrs = (_FP * NERF_N_PARAMS)(*[_fptr(a) for a in arrs])
+    _check(lib.nerf_pack_weights_layout(ptrs, NERF_N_PARAMS, NERF_LAYOUT_ORIGINAL_NERF, f32.ctypes.data_as(_P),
+                                        prm.ctypes.data_as(_P)))
+    del arrs
+    return f32, prm
+
+
 def pack_weights_fp8(sd: Mapping[str, np.ndarray]) -> np.ndarray:
     """Host-only fp8 packing (e4m3 fragments + E8M0 row scales), as the loader runs it."""
     lib = load_library()
@@ -285,6 +306,17 @@ class Device:
         keep, ptrs = _param_list(sd)
         _check(self.lib.nerf_ctx_load_weights(self._ctx, net, ptrs, NERF_N_PARAMS))
         del keep
+        self.loaded.add(net)
+
+    def load_original_nerf(self, net: int, arrays) -> None:
+        """The original NeRF implementation's 24 arrays (weights.original_nerf_tensors), rendered
+        on NERF_FP32 (NERF_LAYOUT_ORIGINAL_NERF)."""
+        from . import weights as W
+
+        arrs = W.original_nerf_tensors(arrays)
+        ptrs = (_FP * NERF_N_PARAMS)(*[_fptr(a) for a in arrs])
+        _check(self.lib.nerf_ctx_load_weights_layout(self._ctx, net, NERF_LAYOUT_ORIGINAL_NERF, ptrs, NERF_N_PARAMS))
+        del arrs
         self.loaded.add(net)
 
     # ---- granular device calls (torch CUDA tensors in, results written in place) ----

@@ -200,3 +200,35 @@ def write_lego_checkpoint(path: str) -> str:
     """The distilled Lego checkpoint in the reference trainer's format (model entries)."""
     coarse, fine = lego_models()
     return save_checkpoint(path, coarse, fine)
+
+
+# ------------------------------------------------ the original NeRF layout --
+def original_nerf_tensors(arrays) -> List[np.ndarray]:
+    """The 24 arrays of the original NeRF implementation's network (the reference's bundled
+    Lego weights, ``data/lego_example_weights/model*_200000.npy``, read by
+    ``tools/lego/npy_static.py``) -> the 22 tensors
+    ``nerf_ctx_load_weights_layout(..., NERF_LAYOUT_ORIGINAL_NERF, ...)`` takes
+    (include/nerf_mi355x.h), in NeRFModel's order and ``[out, in]`` orientation:
+
+    * trunk layer i: ``arrays[2i].T``, ``arrays[2i+1]`` -- layer 4 is [256, 256] and layer 5,
+      whose input is ``cat([pe, h])`` in the original, is [256, 319] with its columns
+      re-ordered to ``[h, pe]`` (exact);
+    * the density head: ``arrays[22].T``, ``arrays[23]`` (alpha, ReLU'd by the renderer);
+    * colour 0: the views layer with the feature layer (linear, no activation) folded in,
+      ``[W_v[:, :256] @ W_f | W_v[:, 256:]]`` and ``W_v[:, :256] @ b_f + b_v`` computed in
+      float64 and rounded once;
+    * colour 1: the rgb layer ``arrays[20].T``, ``arrays[21]``."""
+    a = [np.asarray(x, dtype=np.float64) for x in arrays]
+    if len(a) != 24 or a[10].shape != (HIDDEN + POS_DIM, HIDDEN) or a[22].shape != (HIDDEN, 1):
+        raise ValueError("not the original-NeRF 8x256 layout (24 arrays, skip into layer 5)")
+    out: List[np.ndarray] = []
+    for i in range(8):
+        w = a[2 * i].T
+        if i == 5:   # [pe(63), h(256)] -> [h, pe]
+            w = np.concatenate([w[:, POS_DIM:], w[:, :POS_DIM]], axis=1)
+        out += [w, a[2 * i + 1]]
+    out += [a[22].T, a[23]]
+    w_f, b_f, w_v, b_v = a[16].T, a[17], a[18].T, a[19]
+    out += [np.concatenate([w_v[:, :HIDDEN] @ w_f, w_v[:, HIDDEN:]], axis=1), w_v[:, :HIDDEN] @ b_f + b_v]
+    out += [a[20].T, a[21]]
+    return [np.ascontiguousarray(x, dtype=np.float32) for x in out]

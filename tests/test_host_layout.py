@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
     lib = rt.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.nerf_abi_version() == 5
+    assert lib.nerf_abi_version() == 6
 
 
 def test_uniform_z_bit_exact(golden):
@@ -133,12 +133,16 @@ def heads(prm, x, hcol):
     return sigma, rgb
 
 
-def emulate(f32_blob, bf16_blob, prm, pe, dpe, precision):
+# the original NeRF implementation's trunk (NERF_LAYOUT_ORIGINAL_NERF): the encoding re-enters at layer 5
+LAYERS_ORIG = LAYERS[:4] + [("layers.4", 256, 256, None), ("layers.5", 256, 256, "pos")] + LAYERS[6:]
+
+
+def emulate(f32_blob, bf16_blob, prm, pe, dpe, precision, layers=LAYERS):
     """Run the packed network the way the kernels' lane maps do.  pe [63, n], dpe [27, n]."""
     n = pe.shape[1]
     x = None
     off_f32, off_bf16 = 0, 0
-    for li, (_, out, hidden, extra) in enumerate(LAYERS):
+    for li, (_, out, hidden, extra) in enumerate(layers):
         nt = out // 32
         n_ext = {"pos": 32, "dir": 16, None: 0}[extra]
         ext = [None, None]
@@ -437,3 +441,62 @@ def test_f16x3_packing_splits_and_refuses_out_of_range():
     bad["layers.3.weight"][5, 7] = np.float32(7e4)
     with pytest.raises(rt.NerfError, match="fp16 range"):
         rt.pack_weights_f16x3(bad)
+
+
+def synthetic_original_nerf(seed=0):
+    """24 arrays in the original NeRF implementation's layout ([in, out] kernels; SURVEY §8f
+    row 1), He-scaled so activations stay O(1)."""
+    rng = np.random.default_rng(seed)
+    shapes = ([(63, 256)] + [(256, 256)] * 4 + [(319, 256)] + [(256, 256)] * 2
+              + [(256, 256), (283, 128), (128, 3), (256, 1)])
+    out = []
+    for fan_in, fan_out in shapes:
+        out += [rng.normal(0, np.sqrt(2.0 / fan_in), (fan_in, fan_out)), rng.normal(0, 0.05, fan_out)]
+    return [a.astype(np.float32) for a in out]
+
+
+def original_nerf_direct(a, x, d):
+    """The original network in float64 (the restatement of tools/lego/teacher.py): encodings
+    sin(2^k x) without pi, skip cat([pe, h]) into layer 5, normalised view directions, a linear
+    feature layer before the views layer.  x, d [n, 3] -> sigma [n], rgb [3, n]."""
+    a = [np.asarray(v, np.float64) for v in a]
+
+    def embed(v, L):
+        return np.concatenate([v] + [f(v * 2.0 ** k) for k in range(L) for f in (np.sin, np.cos)], -1)
+
+    pe = embed(x, 10)
+    ve = embed(d / np.linalg.norm(d, axis=-1, keepdims=True), 4)
+    h = pe
+    for i in range(8):
+        h = np.maximum(h @ a[2 * i] + a[2 * i + 1], 0)
+        if i == 4:
+            h = np.concatenate([pe, h], -1)
+    sigma = np.maximum(h @ a[22] + a[23], 0)[:, 0]
+    feat = h @ a[16] + a[17]
+    h2 = np.maximum(np.concatenate([feat, ve], -1) @ a[18] + a[19], 0)
+    return sigma, (1 / (1 + np.exp(-(h2 @ a[20] + a[21])))).T
+
+
+def test_original_nerf_layout_packing_computes_the_network():
+    """NERF_LAYOUT_ORIGINAL_NERF (the optional second weight layout): the host
+    transform (layer 5's columns re-ordered to [h, pe], the feature layer folded into colour 0 in
+    float64) and the packer's skip-at-layer-5 f32 blob, pushed through the fp32 kernel's lane maps
+    with the no-pi encodings of normalised directions, compute the original network."""
+    arrays = synthetic_original_nerf(3)
+    f32, prm = rt.pack_weights_original_nerf(arrays)
+    rng = np.random.default_rng(4)
+    x = rng.uniform(-1.2, 1.2, (20, 3))
+    d = rng.normal(0, 1, (20, 3)) * rng.uniform(0.5, 2.0, (20, 1))      # raw, unnormalised rays_d
+
+    def embed(v, L):
+        return np.concatenate([v] + [f(v * 2.0 ** k) for k in range(L) for f in (np.sin, np.cos)], -1)
+
+    pe = embed(x, 10).T
+    dpe = embed(d / np.linalg.norm(d, axis=-1, keepdims=True), 4).T
+    s_emu, rgb_emu = emulate(f32, None, prm, pe, dpe, "fp32", LAYERS_ORIG)
+    s_dir, rgb_dir = original_nerf_direct(arrays, x, d)
+    assert np.abs(s_dir).max() > 1e-2 and rgb_dir.std() > 1e-3              # a non-degenerate network
+    np.testing.assert_allclose(s_emu, s_dir, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(rgb_emu, rgb_dir, rtol=1e-5, atol=1e-5)
+    # the NeRFModel layout of the same blob sizes: the two layouts differ exactly in layers 4 and 5
+    assert f32.size == rt.pack_weights(W.synthetic_state_dict(1))[0].size
