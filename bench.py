@@ -447,10 +447,10 @@ def int8_renderer_error():
     return {"reference": os.path.relpath(pc, REPO), "views": views}
 
 
-def original_nerf_leg(poses, local):
+def original_nerf_leg(poses, local, precision):
     """The reference's own bundled Lego networks (the original NeRF implementation's layout,
-    data/lego_example_weights) on the fp32 kernel (NERF_LAYOUT_ORIGINAL_NERF):
-    rays/s at 800x600x128 on the suite's two views."""
+    data/lego_example_weights) on the fp32 or split-fp16 kernel
+    (NERF_LAYOUT_ORIGINAL_NERF): rays/s at 800x600x128 on the suite's two views."""
     from nerf_amd import weights as W
     from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
     from tools.lego import teacher as T
@@ -458,15 +458,17 @@ def original_nerf_leg(poses, local):
     if not all(os.path.exists(os.path.join(REPO, "tools", "lego", f"_teacher_{w}.npz")) for w in ("coarse", "fine")) \
             and not os.path.isdir(T.LEGO_DIR):
         return {"error": "tools/lego/_teacher_*.npz missing (written by __graft_entry__.build())"}
-    r = MI355XRenderer("fp32", device_index=local)
+    r = MI355XRenderer(precision, device_index=local)
     r.setup_original_nerf(T.load_arrays("coarse"), T.load_arrays("fine"))
     r.hip.set_profiling(True)
     step, _ = frame_step(r, poses, 800, 600, 128, 0, 1)
     dt = time_steps(step, 1, 2, 1) / len(poses)
     ms = kernel_ms(r, 2 * len(poses))
+    r.check_range()
     flop = 800 * 600 * 128 * W.FLOPS_PER_SAMPLE
     return {"rays_per_s": 800 * 600 / dt, "ms_per_frame": 1e3 * dt, "mlp_kernel_ms": ms,
-            "mlp_frac_f32_peak": flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"],
+            "mlp_frac_of_peak": flop / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[precision],
+            "peak": f"{PEAK_TFLOPS[precision]:.1f} TFLOP/s ({precision})",
             "parity": "tests/test_gpu_lego_original.py: whole 200x150x32 frames and an 800x600x128 band within 1e-4 "
                       "of the same networks restated on the CPU (tools/lego/teacher.py)",
             "network": "original NeRF layout (skip into layer 5, no-pi encodings, normalised view directions, "
@@ -513,7 +515,8 @@ def other_configs(ckpt, poses, local, ref32):
                 "reference on Lego (tests/test_gpu_lego.py, whole 800x600x128 frames) at three f16 MFMAs "
                 "per product; the headline bf16 line meets the roofline clause, not the gate"}
 
-    out["lego_original_nerf_fp32_800x600x128"] = original_nerf_leg(poses, local)
+    out["lego_original_nerf_fp32_800x600x128"] = original_nerf_leg(poses, local, "fp32")
+    out["lego_original_nerf_f16x3_800x600x128"] = original_nerf_leg(poses, local, "f16x3")
 
     h = MI355XRenderer("bf16", n_importance=128, device_index=local)
     h.setup(ckpt)

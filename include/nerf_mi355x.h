@@ -96,8 +96,8 @@ int nerf_ctx_load_weights(nerf_ctx* ctx, int net, const float* const* params, in
  *   three changes the host makes (nerf_amd/weights.py original_nerf_tensors): layers.4 is
  *   [256, 256], layers.5 is [256, 319] with its columns re-ordered to [h, pe], and
  *   color_layers.0 is the views layer with the feature layer folded in (W_v[:, :256] W_f,
- *   bias W_v[:, :256] b_f + b_v, in float64).  Rendered on NERF_FP32 only (other precisions are
- *   refused for such a net). */
+ *   bias W_v[:, :256] b_f + b_v, in float64).  Rendered on NERF_FP32 and NERF_F16X3 (the other
+ *   precisions are refused for such a net). */
 #define NERF_LAYOUT_NERFMODEL 0
 #define NERF_LAYOUT_ORIGINAL_NERF 1
 int nerf_ctx_load_weights_layout(nerf_ctx* ctx, int net, int layout, const float* const* params, int n_params);
@@ -108,9 +108,11 @@ int nerf_ctx_load_weights_layout(nerf_ctx* ctx, int net, int layout, const float
 void nerf_packed_sizes(size_t* f32_blob, size_t* bf16_blob, size_t* param_blob);
 int nerf_pack_weights(const float* const* params, int n_params, float* f32_blob, uint16_t* bf16_blob,
                       float* param_blob);
-/* The f32 and params blobs of a network in either layout (NERF_LAYOUT_*). */
+/* The f32, params and (optional, NULL to skip) NERF_F16X3 blobs of a network in either layout
+ * (NERF_LAYOUT_*); NERF_E_INVALID if the f16x3 blob is asked for and a weight is outside fp16's
+ * range. */
 int nerf_pack_weights_layout(const float* const* params, int n_params, int layout, float* f32_blob,
-                             float* param_blob);
+                             float* param_blob, uint16_t* f16x3_blob);
 
 /* Pure host helpers for the fp8 path: the packed mixed blob the fp8 kernel reads (the fp8
  * layers' e4m3 fragment units, the bf16 units of L0, L1, C0, L4's encoding inputs and the

@@ -118,8 +118,9 @@ int check_net(nerf_ctx* ctx, int net, int precision) {
       precision != NERF_F16X3)
     return set_error(NERF_E_INVALID, "bad precision %d", precision);
   if (!ctx->net[net].loaded) return set_error(NERF_E_NO_WEIGHTS, "%s network not loaded", net ? "fine" : "coarse");
-  if (ctx->net[net].layout == NERF_LAYOUT_ORIGINAL_NERF && precision != NERF_FP32)
-    return set_error(NERF_E_INVALID, "%s network has the original-NeRF layout: NERF_FP32 only", net ? "fine" : "coarse");
+  if (ctx->net[net].layout == NERF_LAYOUT_ORIGINAL_NERF && precision != NERF_FP32 && precision != NERF_F16X3)
+    return set_error(NERF_E_INVALID, "%s network has the original-NeRF layout: NERF_FP32 and NERF_F16X3 only",
+                     net ? "fine" : "coarse");
   if (precision == NERF_F16X3 && !ctx->net[net].f16x3_ok)
     return set_error(NERF_E_INVALID, "%s network has weights outside fp16's range: NERF_F16X3 unavailable",
                      net ? "fine" : "coarse");
@@ -143,7 +144,8 @@ hipError_t run_mlp(nerf_ctx* ctx, int net, int precision, const SampleSrc& src, 
   if (precision == NERF_BF16) return launch_mlp_bf16(nd.bf16, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_FP8) return launch_mlp_fp8(nd.fp8, nd.params, src, n, out, expl, s, seg, wloc);
   if (precision == NERF_BF16X3) return launch_mlp_bf16x3(nd.bf16x3, nd.params, src, n, out, expl, s, seg);
-  if (precision == NERF_F16X3) return launch_mlp_f16x3(nd.f16x3, nd.params, src, n, out, expl, s, seg, ctx->d_range);
+  if (precision == NERF_F16X3)
+    return launch_mlp_f16x3(nd.f16x3, nd.params, src, n, out, expl, s, seg, ctx->d_range, nd.layout);
   return launch_mlp_f32(nd.f32, nd.params, src, n, out, expl, s, nd.layout);
 }
 
@@ -261,15 +263,26 @@ int nerf_ctx_load_weights_layout(nerf_ctx* ctx, int net, int layout, const float
   size_t nf32, nbf16, nprm;
   nerf_packed_sizes(&nf32, &nbf16, &nprm);
   std::vector<float> f32(nf32 / 4), prm(nprm / 4);
-  int rc = nerf_pack_weights_layout(params, n_params, layout, f32.data(), prm.data());
+  int rc = nerf_pack_weights_layout(params, n_params, layout, f32.data(), prm.data(), nullptr);
   if (rc != NERF_OK) return rc;
+  // the split-fp16 blob when every weight fits fp16's range (else NERF_F16X3 stays unavailable)
+  const size_t nx3 = nerf_bf16x3_blob_bytes();
+  std::vector<uint16_t> h3(nx3 / 2);
+  char saved_err[sizeof(g_err)];
+  std::memcpy(saved_err, g_err, sizeof(g_err));
+  const bool have_f16x3 = nerf_pack_weights_layout(params, n_params, layout, nullptr, nullptr, h3.data()) == NERF_OK;
+  if (!have_f16x3) std::memcpy(g_err, saved_err, sizeof(g_err));
   DeviceGuard g(ctx->device);
   NetDev& nd = ctx->net[net];
   if (!nd.f32) HIP_TRY(hipMalloc((void**)&nd.f32, nf32));
   if (!nd.params) HIP_TRY(hipMalloc((void**)&nd.params, nprm));
   HIP_TRY(hipMemcpy(nd.f32, f32.data(), nf32, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(nd.params, prm.data(), nprm, hipMemcpyHostToDevice));
-  nd.f16x3_ok = false;   // the other precisions' blobs (if any) belong to an earlier network
+  if (have_f16x3) {
+    if (!nd.f16x3) HIP_TRY(hipMalloc(&nd.f16x3, nx3));
+    HIP_TRY(hipMemcpy(nd.f16x3, h3.data(), nx3, hipMemcpyHostToDevice));
+  }
+  nd.f16x3_ok = have_f16x3;
   nd.loaded = true;
   nd.layout = layout;
   return NERF_OK;

@@ -5,8 +5,8 @@
 namespace nerf {
 
 hipError_t launch_mlp_f16x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                            bool explicit_points, hipStream_t stream, float* seg, int* range_flag) {
-  return launch_x3<OpF16>(blob, params, src, n_points, out, explicit_points, stream, seg, range_flag);
+                            bool explicit_points, hipStream_t stream, float* seg, int* range_flag, int layout) {
+  return launch_x3<OpF16>(blob, params, src, n_points, out, explicit_points, stream, seg, range_flag, layout);
 }
 
 }  // namespace nerf

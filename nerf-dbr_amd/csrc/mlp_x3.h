@@ -159,7 +159,7 @@ struct UnitInfo {
 struct UnitTable {
   UnitInfo u[kUnits];
 };
-constexpr UnitTable make_unit_table() {
+constexpr UnitTable make_unit_table(int skip = kSkipNeRFModel) {
   UnitTable t{};
   for (int n = 0; n < kUnits; ++n) {
     UnitInfo& x = t.u[n];
@@ -168,9 +168,9 @@ constexpr UnitTable make_unit_table() {
       continue;
     }
     int l = 0;
-    while (l + 1 < kNumMfmaLayers && bf16_unit_base(l + 1) <= n) ++l;
-    const int ks = (n - bf16_unit_base(l)) % ksteps_bf16(l);
-    const int ex = ks < layer_shape(l).hidden / 16 ? 0 : layer_shape(l).extra;
+    while (l + 1 < kNumMfmaLayers && bf16_unit_base(l + 1, skip) <= n) ++l;
+    const int ks = (n - bf16_unit_base(l, skip)) % ksteps_bf16(l, skip);
+    const int ex = ks < layer_shape(l, skip).hidden / 16 ? 0 : layer_shape(l, skip).extra;
     x = UnitInfo{l, ks, ex, 4 + (ex != 0 ? 2 : 0), 0, ks == 0};
   }
   constexpr int kBiasReads = 8;   // 2 tiles x 4 x 16 B
@@ -190,7 +190,10 @@ constexpr UnitTable make_unit_table() {
   }
   return t;
 }
-constexpr UnitTable kTab = make_unit_table();
+// per network layout (nerf_layout.h kSkip*: the layer that takes the position encoding again)
+template <int kSkip>
+constexpr UnitTable kTabT = make_unit_table(kSkip);
+constexpr UnitTable kTab = kTabT<kSkipNeRFModel>;
 
 struct Ctx {
   const char* blob;
@@ -261,8 +264,9 @@ constexpr bool kNoDir = false;
 
 // Reads of unit n into ring entry n % kRing: A_hi and A_lo of the unit's two
 // output tiles and, for encoding inputs, the B fragment's hi and lo.
-template <class Op, class F = typename Op::frag>
+template <class Op, int kSkip = kSkipNeRFModel, class F = typename Op::frag>
 __device__ __forceinline__ void read_unit(const Ctx& cx, int n, F (&ra)[kRing][4], F (&rb)[kRing][2]) {
+  constexpr UnitTable kTab = kTabT<kSkip>;
 #ifdef NERF_X3_ABLATE_NOREAD   // timing-only lab build (wrong results): the ring's first fragments reused
   if (n >= kRing) return;
 #endif
@@ -273,7 +277,7 @@ __device__ __forceinline__ void read_unit(const Ctx& cx, int n, F (&ra)[kRing][4
   for (int f = 0; f < 4; ++f) ra[n % kRing][f] = ds_read_b128<F>(base, off + f * 1024);
   const int ex = kTab.u[n].extra;
   if (ex != 0 && !(kNoDir && ex == kDir)) {
-    const int u = kTab.u[n].kstep - layer_shape(kTab.u[n].layer).hidden / 16;
+    const int u = kTab.u[n].kstep - layer_shape(kTab.u[n].layer, kSkip).hidden / 16;
     if (ex == kPos) {
       rb[n % kRing][0] = ds_read_b128<F>(cx.pe_addr, u * 1024);
       rb[n % kRing][1] = ds_read_b128<F>(cx.pe_addr, 4096 + u * 1024);
@@ -529,15 +533,16 @@ __device__ __forceinline__ void sched_unit_pattern() {
 }
 
 // One layer: reads the previous layer's fragments (ih/il), fills the next's (oh/ol).
-template <int L, bool kTrain, class Op, class F = typename Op::frag>
+template <int L, bool kTrain, class Op, int kSkip = kSkipNeRFModel, class F = typename Op::frag>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x4 (&il)[16], u32x4 (&oh)[16],
                                          u32x4 (&ol)[16], F (&ra)[kRing][4], F (&rb)[kRing][2],
                                          const Ctx& cx, TrainSink& sk, bool& nan_seen) {
-  constexpr LayerShape sh = layer_shape(L);
+  constexpr LayerShape sh = layer_shape(L, kSkip);
+  constexpr UnitTable kTab = kTabT<kSkip>;
   constexpr int KH = sh.hidden / 16;
-  constexpr int KU = ksteps_bf16(L);
+  constexpr int KU = ksteps_bf16(L, kSkip);
   constexpr int NQ = out_tiles(L) / 2;
-  constexpr int N0 = bf16_unit_base(L);
+  constexpr int N0 = bf16_unit_base(L, kSkip);
   constexpr bool kConvert = L != L0;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -546,7 +551,7 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
       const int n = N0 + q * KU + u;
       seam_before<kTrain>(cx, n);
       if (u == 0) issue_bias(cx, L, q, acc);
-      if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
+      if (n + kPf < kUnits) read_unit<Op, kSkip>(cx, n + kPf, ra, rb);
       wait_lgkm(kTab.u[n].lgkm);
       __builtin_amdgcn_sched_barrier(0);
       const bool hid = u < KH;
@@ -577,13 +582,18 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[8], u32x4 (&ih)[16], u32x
 
 // seg != nullptr (render passes, S % 32 == 0): one segment record per wave's 32
 // samples instead of out's (sigma, r, g, b).
-template <bool kExplicit, bool kTrain, class Op>
+// kOrig: the original NeRF implementation's network (NERF_LAYOUT_ORIGINAL_NERF, render and
+// query only): position encoding again at layer 5, encodings without pi, view directions
+// normalised before their encoding (mlp_f32.hip, nerf_layout.h).
+template <bool kExplicit, bool kTrain, class Op, bool kOrig = false>
 __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restrict__ blob,
                                                              const float* __restrict__ prm_g, SampleSrc src,
                                                              long n_points, f32x4* __restrict__ out,
                                                              f32x4* __restrict__ seg, X3TrainOut tro,
                                                              int* __restrict__ range_flag) {
   typedef typename Op::frag F;
+  static_assert(!(kOrig && kTrain), "the original-NeRF layout renders only");
+  constexpr int S = kOrig ? kSkipOriginal : kSkipNeRFModel;
   __shared__ __attribute__((aligned(16))) char lds[kTrain ? kLdsBytesTrain : kLdsBytes];
   const int lane = threadIdx.x & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -645,8 +655,14 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
       } else {
         fetch_sample<kExplicit>(src, pc, x, d);
       }
-      pos_encode<false, kTrain>(x[0], x[1], x[2], h, pef);    // accurate sin/cos, as the fp32 path
-      if (!kNoDir) dir_encode<false, kTrain>(d[0], d[1], d[2], h, def);
+      pos_encode<false, kTrain, kOrig>(x[0], x[1], x[2], h, pef);    // accurate sin/cos, as the fp32 path
+      if (kOrig) {   // the original's viewdirs = rays_d / |rays_d| (its encoding input)
+        const float nd = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d[0], d[0]), __fmul_rn(d[1], d[1])),
+                                              __fmul_rn(d[2], d[2])));
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = __fdiv_rn(d[c], nd);
+      }
+      if (!kNoDir) dir_encode<false, kTrain, kOrig>(d[0], d[1], d[2], h, def);
       char* pe_dst = lds + kLdsPeOff + wave_u * kPeWaveB + lane * 16;
       char* de_dst = lds + kLdsDeOff + wave_u * kDeWaveB + lane * 16;
 #pragma unroll
@@ -677,19 +693,19 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     F ra[kRing][4], rb[kRing][2];
     f32x16 acc[8];
 #pragma unroll
-    for (int n = 0; n < kPf; ++n) read_unit<Op>(cx, n, ra, rb);
+    for (int n = 0; n < kPf; ++n) read_unit<Op, S>(cx, n, ra, rb);
 
     u32x4 aH[16], aL[16], bH[16], bL[16];
     bool nan_seen = false;
-    layer_x3<L0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
-    layer_x3<L1, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
-    layer_x3<L2, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
-    layer_x3<L3, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
-    layer_x3<L4, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);   // skip: [x, pe] (nerf.py:109-110)
-    layer_x3<L5, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
-    layer_x3<L6, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
-    layer_x3<L7, kTrain, Op>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
-    layer_x3<C0, kTrain, Op>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);   // [x, PE4(d)] (nerf.py:117-121)
+    layer_x3<L0, kTrain, Op, S>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L1, kTrain, Op, S>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L2, kTrain, Op, S>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L3, kTrain, Op, S>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L4, kTrain, Op, S>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);   // skip: [x, pe] (nerf.py:109-110)
+    layer_x3<L5, kTrain, Op, S>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L6, kTrain, Op, S>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);
+    layer_x3<L7, kTrain, Op, S>(acc, aH, aL, bH, bL, ra, rb, cx, sk, nan_seen);
+    layer_x3<C0, kTrain, Op, S>(acc, bH, bL, aH, aL, ra, rb, cx, sk, nan_seen);   // [x, PE4(d)] (nerf.py:117-121)
 
     // Heads (nerf.py:114, 123-129): one tile, density row 3 over L7's fragments
     // (bH/bL, C0's input, k-steps 0..15), colour rows 0-2 over C0's output
@@ -705,7 +721,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
     for (int i = 0; i < kHeadUnits; ++i) {
       const int n = kHeadUnitBase + i;
       seam_before<kTrain>(cx, n);
-      if (n + kPf < kUnits) read_unit<Op>(cx, n + kPf, ra, rb);
+      if (n + kPf < kUnits) read_unit<Op, S>(cx, n + kPf, ra, rb);
       wait_lgkm(4 * (kUnits - 1 - n < kPf ? kUnits - 1 - n : kPf) + seam_writes_since(n));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -753,7 +769,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_x3_kernel(const char* __restr
 // render-pass kernel, so a variant compiles in a fifth of the time.
 template <class Op>
 hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src, long n_points, float* out,
-                     bool explicit_points, hipStream_t stream, float* seg, int* range_flag) {
+                     bool explicit_points, hipStream_t stream, float* seg, int* range_flag, int layout = 0) {
 #ifdef NERF_X3_LAB
   if (explicit_points || !__is_same(Op, OpF16)) return hipErrorNotSupported;
 #endif
@@ -762,6 +778,21 @@ hipError_t launch_x3(const void* blob, const float* params, const SampleSrc& src
   const long tiles = (n_points + kSamplesPerBlock - 1) / kSamplesPerBlock;
   const long blocks = tiles < current_device_cus() ? tiles : current_device_cus();   // one workgroup per CU
   const dim3 grid{unsigned(blocks), 1, 1}, block{kThreads, 1, 1};
+  if (layout != 0) {   // NERF_LAYOUT_ORIGINAL_NERF: the split-fp16 unit only
+#ifndef NERF_X3_LAB
+    if constexpr (__is_same(Op, OpF16)) {
+      if (layout != 1) return hipErrorInvalidValue;
+      if (explicit_points)
+        hipLaunchKernelGGL((mlp_x3_kernel<true, false, Op, true>), grid, block, 0, stream, (const char*)blob, params,
+                           src, n_points, (f32x4*)out, (f32x4*)nullptr, X3TrainOut{}, range_flag);
+      else
+        hipLaunchKernelGGL((mlp_x3_kernel<false, false, Op, true>), grid, block, 0, stream, (const char*)blob, params,
+                           src, n_points, (f32x4*)out, (f32x4*)seg, X3TrainOut{}, range_flag);
+      return hipGetLastError();
+    }
+#endif
+    return hipErrorNotSupported;
+  }
 #ifndef NERF_X3_LAB
   if (explicit_points)
     hipLaunchKernelGGL((mlp_x3_kernel<true, false, Op>), grid, block, 0, stream, (const char*)blob, params, src,

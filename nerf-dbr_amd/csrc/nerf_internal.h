@@ -45,7 +45,7 @@ hipError_t launch_mlp_bf16x3(const void* blob, const float* params, const Sample
 // range_flag: set to 1 (device int) when a sample's activation overflowed fp16 (mlp_x3.h).
 hipError_t launch_mlp_f16x3(const void* blob, const float* params, const SampleSrc& src, long n_points,
                             float* out, bool explicit_points, hipStream_t stream, float* seg = nullptr,
-                            int* range_flag = nullptr);
+                            int* range_flag = nullptr, int layout = 0);
 // The same kernel as the training forward (train.hip): per sample also every trunk layer's
 // post-ReLU row h[l] [P][256] and ReLU bit words mb[l] [P][8], the colour-0 row and density
 // hc [P][132], and (r, g, b, sigma) rgbs [P][4]; blob is the split-bf16 blob of the net's

@@ -88,7 +88,10 @@ NL_HD int ksteps_f32(int l, int skip = kSkipNeRFModel) {
   LayerShape s = layer_shape(l, skip);
   return s.hidden / 2 + extra_slots(s.extra);
 }
-NL_HD int ksteps_bf16(int l) { LayerShape s = layer_shape(l); return s.hidden / 16 + extra_slots(s.extra) / 8; }
+NL_HD int ksteps_bf16(int l, int skip = kSkipNeRFModel) {
+  LayerShape s = layer_shape(l, skip);
+  return s.hidden / 16 + extra_slots(s.extra) / 8;
+}
 
 // Reference column index of the weight that multiplies the value lane half h
 // supplies at (k-step u, element j) -- or -1 for padding.
@@ -100,8 +103,8 @@ NL_HD int f32_k_col(int l, int u, int h, int skip = kSkipNeRFModel) {
   int f = s.extra == kPos ? pe_slot_feature(h, q) : dpe_slot_feature(h, q);
   return f < 0 ? -1 : s.hidden + f;
 }
-NL_HD int bf16_k_col(int l, int u, int h, int j) {
-  LayerShape s = layer_shape(l);
+NL_HD int bf16_k_col(int l, int u, int h, int j, int skip = kSkipNeRFModel) {
+  LayerShape s = layer_shape(l, skip);
   int nh = s.hidden / 16;
   if (u < nh) return hid_bf16_feature(u, h, j);
   int q = 8 * (u - nh) + j;
@@ -135,10 +138,10 @@ constexpr int kUnitBytes = 2048;                    // one k-step of one quarter
 constexpr int kUnitsPerChunk = kChunkBytes / kUnitBytes;
 
 NL_HD int f32_layer_floats(int l, int skip = kSkipNeRFModel) { return ksteps_f32(l, skip) * out_tiles(l) * 64; }
-NL_HD int bf16_layer_units(int l) { return (out_tiles(l) / 2) * ksteps_bf16(l); }
-NL_HD int bf16_unit_base(int l) {                   // first unit of layer l
+NL_HD int bf16_layer_units(int l, int skip = kSkipNeRFModel) { return (out_tiles(l) / 2) * ksteps_bf16(l, skip); }
+NL_HD int bf16_unit_base(int l, int skip = kSkipNeRFModel) {   // first unit of layer l
   int n = 0;
-  for (int i = 0; i < l; ++i) n += bf16_layer_units(i);
+  for (int i = 0; i < l; ++i) n += bf16_layer_units(i, skip);
   return n;
 }
 NL_HD int f32_blob_floats() {

@@ -65,18 +65,19 @@ int row_scale_exp(float max_abs) {
 // The bf16 blob's values before rounding (fp32), in stream order: per layer
 // [quarter][k-step][tile-in-quarter][lane][8], then the heads' tile
 // (nerf_layout.h); padding slots are 0.
-void bf16_stream_values(const float* const* params, std::vector<float>& out) {
-  auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * kSpecIn[spec] + k]; };
+void bf16_stream_values(const float* const* params, std::vector<float>& out, int skip = kSkipNeRFModel) {
+  const int* in = skip == kSkipOriginal ? kSpecInOrig : kSpecIn;
+  auto W = [&](int spec, int o, int k) { return params[2 * spec][size_t(o) * in[spec] + k]; };
   out.clear();
   out.reserve(size_t(kBf16BlobBytes) / 2);
   for (int l = 0; l < kNumMfmaLayers; ++l) {
-    const int spec = kSpecOfLayer[l], nq = out_tiles(l) / 2, ku = ksteps_bf16(l);
+    const int spec = kSpecOfLayer[l], nq = out_tiles(l) / 2, ku = ksteps_bf16(l, skip);
     for (int q = 0; q < nq; ++q)
       for (int u = 0; u < ku; ++u)
         for (int o2 = 0; o2 < 2; ++o2)
           for (int lane = 0; lane < 64; ++lane)
             for (int j = 0; j < 8; ++j) {
-              const int col = bf16_k_col(l, u, lane >> 5, j);
+              const int col = bf16_k_col(l, u, lane >> 5, j, skip);
               const int row = 32 * (2 * q + o2) + (lane & 31);
               out.push_back(col < 0 ? 0.0f : W(spec, row, col));
             }
@@ -117,13 +118,10 @@ extern "C" int nerf_pack_weights_bf16x3(const float* const* params, int n_params
   return NERF_OK;
 }
 
-extern "C" int nerf_pack_weights_f16x3(const float* const* params, int n_params, uint16_t* blob) {
-  if (!params || n_params != NERF_N_PARAMS || !blob)
-    return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: need %d tensors and a blob", NERF_N_PARAMS);
-  for (int i = 0; i < NERF_N_PARAMS; ++i)
-    if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: tensor %d is NULL", i);
+namespace {
+int pack_f16x3(const float* const* params, int skip, uint16_t* blob) {
   std::vector<float> vals;
-  bf16_stream_values(params, vals);
+  bf16_stream_values(params, vals, skip);
   constexpr size_t kUnit = size_t(kUnitBytes) / 2;          // 16-bit elements per unit
   std::memset(blob, 0, size_t(kBf16x3BlobBytes));
   for (size_t i = 0; i < vals.size(); ++i) {
@@ -136,6 +134,15 @@ extern "C" int nerf_pack_weights_f16x3(const float* const* params, int n_params,
     std::memcpy(&blob[(2 * unit + 1) * kUnit + off], &lo, 2);
   }
   return NERF_OK;
+}
+}  // namespace
+
+extern "C" int nerf_pack_weights_f16x3(const float* const* params, int n_params, uint16_t* blob) {
+  if (!params || n_params != NERF_N_PARAMS || !blob)
+    return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: need %d tensors and a blob", NERF_N_PARAMS);
+  for (int i = 0; i < NERF_N_PARAMS; ++i)
+    if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_f16x3: tensor %d is NULL", i);
+  return pack_f16x3(params, kSkipNeRFModel, blob);
 }
 
 extern "C" size_t nerf_fp8_blob_bytes(void) { return size_t(kFp8BlobBytes); }
@@ -238,15 +245,22 @@ void pack_f32(const float* const* params, int skip, float* f32_blob) {
 }  // namespace
 
 extern "C" int nerf_pack_weights_layout(const float* const* params, int n_params, int layout, float* f32_blob,
-                                        float* param_blob) {
+                                        float* param_blob, uint16_t* f16x3_blob) {
   if (layout != NERF_LAYOUT_NERFMODEL && layout != NERF_LAYOUT_ORIGINAL_NERF)
     return set_error(NERF_E_INVALID, "nerf_pack_weights_layout: unknown layout %d", layout);
-  if (layout == NERF_LAYOUT_NERFMODEL) return nerf_pack_weights(params, n_params, f32_blob, nullptr, param_blob);
+  if (layout == NERF_LAYOUT_NERFMODEL) {
+    const int rc = nerf_pack_weights(params, n_params, f32_blob, nullptr, param_blob);
+    return rc != NERF_OK || !f16x3_blob ? rc : nerf_pack_weights_f16x3(params, n_params, f16x3_blob);
+  }
   if (!params || n_params != NERF_N_PARAMS)
     return set_error(NERF_E_INVALID, "nerf_pack_weights_layout: need %d tensors, got %d", NERF_N_PARAMS, n_params);
   for (int i = 0; i < NERF_N_PARAMS; ++i)
     if (!params[i]) return set_error(NERF_E_INVALID, "nerf_pack_weights_layout: tensor %d is NULL", i);
   if (f32_blob) pack_f32(params, kSkipOriginal, f32_blob);
+  if (f16x3_blob) {
+    const int rc = pack_f16x3(params, kSkipOriginal, f16x3_blob);
+    if (rc != NERF_OK) return rc;
+  }
   // the params blob reads only biases, the density head and colour-1: the same in both layouts
   return param_blob ? nerf_pack_weights(params, n_params, nullptr, nullptr, param_blob) : NERF_OK;
 }

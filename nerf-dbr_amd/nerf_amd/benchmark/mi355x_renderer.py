@@ -93,10 +93,11 @@ class MI355XRenderer(BaseUnifiedRenderer):
     def setup_original_nerf(self, coarse_arrays, fine_arrays) -> None:
         """Instead of ``setup``: the original NeRF implementation's networks (the 24 arrays each
         of the reference's bundled ``data/lego_example_weights``), rendered
-        with this renderer's path and semantics on the fp32 kernel (include/nerf_mi355x.h
-        NERF_LAYOUT_ORIGINAL_NERF).  Not part of the reference's plugin interface."""
-        if self.precision != "fp32":
-            raise ValueError("the original-NeRF layout renders on fp32 only")
+        with this renderer's path and semantics on the fp32 or the split-fp16 kernel
+        (include/nerf_mi355x.h NERF_LAYOUT_ORIGINAL_NERF).  Not part of the reference's plugin
+        interface."""
+        if self.precision not in ("fp32", "f16x3"):
+            raise ValueError("the original-NeRF layout renders on fp32 and f16x3 only")
         self.hip.load_original_nerf(rt.NERF_NET_COARSE, coarse_arrays)
         self.hip.load_original_nerf(rt.NERF_NET_FINE, fine_arrays)
 

@@ -47,7 +47,7 @@ SIGNATURES = {
     "nerf_device_name": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_int]),
     "nerf_ctx_load_weights": (_c.c_int, [_P, _c.c_int, _c.POINTER(_FP), _c.c_int]),
     "nerf_ctx_load_weights_layout": (_c.c_int, [_P, _c.c_int, _c.c_int, _c.POINTER(_FP), _c.c_int]),
-    "nerf_pack_weights_layout": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _c.c_int, _P, _P]),
+    "nerf_pack_weights_layout": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _c.c_int, _P, _P, _P]),
     "nerf_packed_sizes": (None, [_c.POINTER(_c.c_size_t)] * 3),
     "nerf_pack_weights": (_c.c_int, [_c.POINTER(_FP), _c.c_int, _P, _P, _P]),
     "nerf_uniform_z": (None, [_FP, _c.c_int, _c.c_float, _c.c_float, _FP]),
@@ -198,7 +198,7 @@ def pack_weights_original_nerf(arrays):
     arrs = W.original_nerf_tensors(arrays)
     ptrs = (_FP * NERF_N_PARAMS)(*[_fptr(a) for a in arrs])
     _check(lib.nerf_pack_weights_layout(ptrs, NERF_N_PARAMS, NERF_LAYOUT_ORIGINAL_NERF, f32.ctypes.data_as(_P),
-                                        prm.ctypes.data_as(_P)))
+                                        prm.ctypes.data_as(_P), None))
     del arrs
     return f32, prm
 
@@ -310,7 +310,7 @@ class Device:
 
     def load_original_nerf(self, net: int, arrays) -> None:
         """The original NeRF implementation's 24 arrays (weights.original_nerf_tensors), rendered
-        on NERF_FP32 (NERF_LAYOUT_ORIGINAL_NERF)."""
+        on NERF_FP32 or NERF_F16X3 (NERF_LAYOUT_ORIGINAL_NERF)."""
         from . import weights as W
 
         arrs = W.original_nerf_tensors(arrays)
