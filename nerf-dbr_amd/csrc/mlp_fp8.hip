@@ -113,7 +113,19 @@ constexpr int kEncWaveB = 6 * 1024;
 constexpr int kDirEncOff = 4 * 1024;
 constexpr int kLdsEncOff = kLdsRingOff + kSlots * kChunkB;
 constexpr int kLdsSegOff = kLdsEncOff + kWaves * kCols * kEncWaveB;   // fused compositing: (dist, z) per sample
-constexpr int kLdsBytes = kLdsSegOff + kWaves * kCols * kSamplesPerWave * 8;
+// NERF_FP8_PIPE_ENC (lab knob, 4 waves): the next tile's samples are fetched and encoded during
+// this tile's head units (their MFMAs hide the encoding VALU; the tile top then only seams),
+// the (dist, z) slots double-buffered by tile parity.  Unit of the head loop that fetches, and
+// the two that encode column 0 and 1:
+#ifndef NERF_FP8_PIPE_ENC
+#define NERF_FP8_PIPE_ENC 0
+#endif
+#ifndef NERF_FP8_PIPE_FETCH_UNIT
+#define NERF_FP8_PIPE_FETCH_UNIT 0
+#endif
+static_assert(!NERF_FP8_PIPE_ENC || kCols == 2, "the pipelined encodings assume the two-column form");
+constexpr int kSegBufB = kWaves * kCols * kSamplesPerWave * 8;
+constexpr int kLdsBytes = kLdsSegOff + (NERF_FP8_PIPE_ENC ? 2 : 1) * kSegBufB;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kFp8ScaleBytes % 16 == 0 && kLdsScaleOff % 16 == 0, "16-B aligned carve");
 
@@ -463,17 +475,23 @@ __device__ __forceinline__ void layer_mix(f32x16 (&acc)[kCols][8], i32x8 (&b8in)
   }
 }
 
-// This tile's sample inputs -> its encodings in the wave's own LDS slots (bf16), and for
-// fused compositing the integral's network-independent inputs.
+// A sample's network inputs, and for fused compositing the integral's network-independent ones.
+struct SampleIn {
+  float x[3], d[3], dist, zz;
+};
 template <bool kExplicit>
-__device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src, long p, long n_points, bool fused,
-                                            int col) {
-  float x[3], d[3], pef[32], def[16];
-  float dist = 0.0f, zz = 0.0f;
-  if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, x, d);
-  else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, fused, x, d, dist, zz);
-  pos_encode<true>(x[0], x[1], x[2], cx.h, pef);
-  dir_encode<true>(d[0], d[1], d[2], cx.h, def);
+__device__ __forceinline__ void fetch_in(const SampleSrc& src, long p, long n_points, bool fused, SampleIn& si) {
+  si.dist = 0.0f;
+  si.zz = 0.0f;
+  if (kExplicit) fetch_sample<true>(src, p < n_points ? p : n_points - 1, si.x, si.d);
+  else fetch_render_sample(src, p < n_points ? p : n_points - 1, n_points <= 0xFFFFFFFFL, fused, si.x, si.d, si.dist, si.zz);
+}
+// -> the encodings in the wave's own LDS slots of column col (bf16), (dist, z) into seg buffer sb
+template <bool kExplicit>
+__device__ __forceinline__ void encode_write(const Ctx& cx, const SampleIn& si, bool fused, int col, int sb) {
+  float pef[32], def[16];
+  pos_encode<true>(si.x[0], si.x[1], si.x[2], cx.h, pef);
+  dir_encode<true>(si.d[0], si.d[1], si.d[2], cx.h, def);
   const int slot = cx.wave_u * kCols + col;                 // the column's encoding and segment slots
   char* dst = cx.lds + kLdsEncOff + slot * kEncWaveB + cx.lane * 16;
 #pragma unroll
@@ -491,7 +509,16 @@ __device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src,
     *(bf16x8*)(dst + kDirEncOff + u * 1024) = v;
   }
   if (!kExplicit && fused && cx.h == 0)
-    *(f32x2_t*)(cx.lds + kLdsSegOff + (slot * kSamplesPerWave + (cx.lane & 31)) * 8) = f32x2_t{dist, zz};
+    *(f32x2_t*)(cx.lds + kLdsSegOff + sb * kSegBufB + (slot * kSamplesPerWave + (cx.lane & 31)) * 8) =
+        f32x2_t{si.dist, si.zz};
+}
+// This tile's sample inputs -> its encodings (and (dist, z)), at the tile top.
+template <bool kExplicit>
+__device__ __forceinline__ void encode_tile(const Ctx& cx, const SampleSrc& src, long p, long n_points, bool fused,
+                                            int col, int sb) {
+  SampleIn si;
+  fetch_in<kExplicit>(src, p, n_points, fused, si);
+  encode_write<kExplicit>(cx, si, fused, col, sb);
 }
 
 // A tile's outputs, stored after the next tile's first seam: vmcnt counts stores together
@@ -550,11 +577,13 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
     const long p = (tile * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
     // this tile's encodings into the wave's own slots (its reads of the previous tile's
     // were consumed by that tile's MFMAs)
+    const int sb = NERF_FP8_PIPE_ENC ? int(it & 1) : 0;   // this tile's (dist, z) buffer
 #ifdef NERF_FP8_ABLATE_PE_ONCE
     if (it == 0)
 #endif
+    if (!NERF_FP8_PIPE_ENC || it == 0)   // (pipelined: the previous tile's head units encoded this one)
 #pragma unroll 1
-    for (int c = 0; c < kCols; ++c) encode_tile<kExplicit>(cx, src, p + c * kSamplesPerWave, n_points, fused, c);
+      for (int c = 0; c < kCols; ++c) encode_tile<kExplicit>(cx, src, p + c * kSamplesPerWave, n_points, fused, c, sb);
     if (it == 0) {
       // barrier instance 0 publishes chunk 0 (and the parameters); the lagging half then
       // takes its seam for chunk 0 (instance 1, staging chunk 2)
@@ -599,11 +628,22 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
         hacc[c][3] = prm[kSigB];
       }
     }
+    const long next_tile = tile + gridDim.x;
+    const bool has_next = NERF_FP8_PIPE_ENC && next_tile < n_tiles;   // wave-uniform
+    SampleIn sn[kCols];
 #pragma unroll
     for (int i = 0; i < kMixHeadUnits; ++i) {
       const int n = kMixLayerUnits + i;
       seam_before(cx, n);
       if (n + kPf < kUnits) read_unit(cx, n + kPf, ra, rb);
+      if (NERF_FP8_PIPE_ENC && has_next) {
+        const long pn = (next_tile * kWaves + wave_u) * (kCols * kSamplesPerWave) + (lane & 31);
+        if (i == NERF_FP8_PIPE_FETCH_UNIT)
+#pragma unroll
+          for (int c = 0; c < kCols; ++c) fetch_in<kExplicit>(src, pn + c * kSamplesPerWave, n_points, fused, sn[c]);
+        if (i == 2) encode_write<kExplicit>(cx, sn[0], fused, 0, sb ^ 1);
+        if (i == 4) encode_write<kExplicit>(cx, sn[1], fused, 1, sb ^ 1);
+      }
       wait_lgkm(0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -631,7 +671,7 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fp8_kernel(const char* __rest
       const f32x4 res{relu(hacc[c][3]), sigmoid_ref(hacc[c][0]), sigmoid_ref(hacc[c][1]), sigmoid_ref(hacc[c][2])};
       pd[c] = Pending{};
       if (fused) {                                       // fused compositing: one record per segment
-        const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff +
+        const f32x2_t in = *(const f32x2_t*)(lds + kLdsSegOff + sb * kSegBufB +
                                              ((wave_u * kCols + c) * kSamplesPerWave + (lane_o & 31)) * 8);
         float wl;
         pd[c].v = seg_composite(res, in[0], in[1], lane_o, wl);
