@@ -253,3 +253,18 @@ def test_coarse_precision_option_samples_like_that_precision(ckpt, golden):
           f"rgb {er:.3e} depth {ed:.3e}")
     assert torch.equal(zs[0], zs[1])
     assert er < TOL and ed < TOL
+
+
+def test_coarse_precision_option_rejects_bad_values(ckpt):
+    """NERF_OPT_COARSE_PRECISION takes -1 or a precision (NERF_E_INVALID otherwise), and a
+    renderer built with an unknown coarse precision is refused before any device call."""
+    from nerf_amd import runtime as rt
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+
+    r = renderer(ckpt, "f16x3", "fp32")
+    for bad in (-2, 5, 99):
+        with pytest.raises(rt.NerfError, match="NERF_OPT_COARSE_PRECISION"):
+            r.hip.set_coarse_precision(bad)
+    r.hip.set_coarse_precision(rt.NERF_FP32)       # restore the cached renderer's setting
+    with pytest.raises(ValueError):
+        MI355XRenderer("f16x3", n_importance=NI, coarse_precision="fp16")

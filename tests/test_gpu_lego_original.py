@@ -119,3 +119,28 @@ def test_original_nerf_hierarchical_runs_and_other_precisions_refused():
     out = torch.empty(32, 4, device="cuda")
     with pytest.raises(rt.NerfError, match="original-NeRF layout"):
         r.hip.query(rt.NERF_NET_FINE, rt.NERF_BF16, pos, pos + 1.0, out)
+
+
+def test_original_nerf_hierarchical_f16x3_with_fp32_coarse_samples_like_fp32():
+    """The original networks, 64 + 128: f16x3 with its coarse pass in fp32 takes the fp32 render's
+    fine samples bit for bit, and its image is within the gate of the fp32 render."""
+    from nerf_amd.benchmark.mi355x_renderer import MI355XRenderer
+    from nerf_amd.benchmark.benchmark_suite import generate_test_poses
+
+    pose = generate_test_poses(2)[0]
+    w, h = 120, 90
+    a = MI355XRenderer("f16x3", n_importance=128, coarse_precision="fp32")
+    a.setup_original_nerf(arrays("coarse"), arrays("fine"))
+    b = renderer("fp32", 128)
+    zs, imgs = [], []
+    for r in (a, b):
+        rgb, dep = [t.clone() for t in r.render_image(pose, (w, h), 64)]
+        z = torch.empty(w * h, 192, dtype=torch.float32, device="cuda")
+        r.hip.last_fine_z(w * h, 192, z)
+        zs.append(z.cpu())
+        imgs.append((rgb.cpu(), dep.cpu()))
+    er = float((imgs[0][0] - imgs[1][0]).abs().max())
+    ed = float((imgs[0][1] - imgs[1][1]).abs().max())
+    print(f"original-NeRF 64+128 {w}x{h}: f16x3 (fp32 coarse) vs fp32: fine z equal {bool(torch.equal(zs[0], zs[1]))}, "
+          f"rgb {er:.3e} depth {ed:.3e}")
+    assert torch.equal(zs[0], zs[1]) and er < TOL and ed < TOL
